@@ -1,0 +1,25 @@
+"""hysteria_amd -- Hysteria's Salamander packet obfuscation (extras/obfs) on AMD MI355X.
+
+The product is ``libhyobfs.so`` (gfx950 HIP kernels behind the C ABI of
+``include/hyobfs.h``); this package is its Python host binding.
+"""
+from .salamander import (  # noqa: F401
+    SM_KEY_LEN,
+    SM_PSK_MIN_LEN,
+    SM_SALT_LEN,
+    UDP_BUFFER_SIZE,
+    PSKTooShortError,
+    SalamanderObfuscator,
+    device_count,
+    new_salamander_obfuscator,
+    synth_bimodal_lengths,
+    synth_stream,
+    synth_u64,
+    workspace_size,
+)
+
+__all__ = [
+    "SM_KEY_LEN", "SM_PSK_MIN_LEN", "SM_SALT_LEN", "UDP_BUFFER_SIZE", "PSKTooShortError",
+    "SalamanderObfuscator", "device_count", "new_salamander_obfuscator", "synth_bimodal_lengths",
+    "synth_stream", "synth_u64", "workspace_size",
+]

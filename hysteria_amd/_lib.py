@@ -1,0 +1,116 @@
+"""ctypes binding of libhyobfs.so (include/hyobfs.h).
+
+The library holds the gfx950 kernels; there is no CPU fallback.  If the .so is
+missing or does not load, importing the product API raises immediately.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libhyobfs.so")
+HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "hyobfs.h")
+
+HYOBFS_OK = 0
+HYOBFS_ERR_PSK_TOO_SHORT = -1
+HYOBFS_ERR_INVALID = -2
+HYOBFS_ERR_HIP = -3
+HYOBFS_ERR_NOMEM = -4
+HYOBFS_ERR_NO_DEVICE = -5
+HYOBFS_ERR_IO = -6
+
+
+class HyobfsBatch(ctypes.Structure):
+    """struct hyobfs_batch (include/hyobfs.h)."""
+
+    _fields_ = [
+        ("n", ctypes.c_uint64),
+        ("in_", ctypes.c_void_p),
+        ("in_off", ctypes.c_void_p),
+        ("in_stride", ctypes.c_uint64),
+        ("in_len", ctypes.c_void_p),
+        ("len_uniform", ctypes.c_uint32),
+        ("pkt_cap", ctypes.c_uint32),
+        ("salts", ctypes.c_void_p),
+        ("out", ctypes.c_void_p),
+        ("out_cap", ctypes.c_uint64),
+        ("out_stride", ctypes.c_uint64),
+        ("out_off", ctypes.c_void_p),
+        ("out_len", ctypes.c_void_p),
+        ("out_total", ctypes.c_void_p),
+        ("workspace", ctypes.c_void_p),
+        ("workspace_bytes", ctypes.c_uint64),
+    ]
+
+
+def header_functions(path: str = HEADER_PATH) -> list[str]:
+    """Names of every function declared in include/*.h."""
+    names = []
+    inc = os.path.dirname(path)
+    for fn in sorted(os.listdir(inc)):
+        if not fn.endswith(".h"):
+            continue
+        text = open(os.path.join(inc, fn)).read()
+        text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+        names += re.findall(r"\b(hyobfs_[a-z0-9_]+)\s*\(", text)
+    return sorted(set(names))
+
+
+_lib = None
+
+
+def load(path: str = LIB_PATH) -> ctypes.CDLL:
+    """Load libhyobfs.so and declare the ABI.  Raises OSError if it is missing."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise OSError(f"{path} is missing: build it with `make -C hysteria_amd/csrc` "
+                      "(or __graft_entry__.build()); there is no CPU fallback")
+    lib = ctypes.CDLL(path)
+    vp, sz, u64, u32, i32 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int
+    pctx = ctypes.c_void_p
+    sig = {
+        "hyobfs_abi_version": (i32, []),
+        "hyobfs_status_string": (ctypes.c_char_p, [i32]),
+        "hyobfs_device_count": (i32, []),
+        "hyobfs_salamander_new": (i32, [vp, sz, i32, ctypes.POINTER(ctypes.c_void_p)]),
+        "hyobfs_salamander_free": (None, [pctx]),
+        "hyobfs_salamander_device": (i32, [pctx]),
+        "hyobfs_salamander_seed": (None, [pctx, u64]),
+        "hyobfs_salamander_next_salts": (None, [pctx, vp, sz]),
+        "hyobfs_salamander_key": (i32, [pctx, vp, vp]),
+        "hyobfs_salamander_keys_batch": (i32, [pctx, vp, vp, u64, vp]),
+        "hyobfs_salamander_obfuscate": (sz, [pctx, vp, sz, vp, vp, sz]),
+        "hyobfs_salamander_obfuscate_auto": (sz, [pctx, vp, sz, vp, sz]),
+        "hyobfs_salamander_deobfuscate": (sz, [pctx, vp, sz, vp, sz]),
+        "hyobfs_batch_workspace_size": (u64, [u64]),
+        "hyobfs_salamander_obfuscate_batch": (i32, [pctx, ctypes.POINTER(HyobfsBatch), vp]),
+        "hyobfs_salamander_deobfuscate_batch": (i32, [pctx, ctypes.POINTER(HyobfsBatch), vp]),
+        "hyobfs_synth_stream": (i32, [vp, u64, u64, u64, vp]),
+        "hyobfs_synth_u64": (i32, [vp, u64, u64, u64, vp]),
+        "hyobfs_synth_bimodal_lengths": (i32, [vp, u64, u64, u64, vp]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(lib, name)
+        f.restype = res
+        f.argtypes = args
+    _lib = lib
+    return lib
+
+
+def status_string(st: int) -> str:
+    return load().hyobfs_status_string(st).decode()
+
+
+class HyobfsError(RuntimeError):
+    def __init__(self, status: int, what: str = ""):
+        self.status = status
+        super().__init__(f"{what}: {status_string(status)} ({status})" if what else status_string(status))
+
+
+def check(status: int, what: str = "") -> None:
+    if status != HYOBFS_OK:
+        raise HyobfsError(status, what)

@@ -1,0 +1,442 @@
+// hyobfs_api.cpp -- the C ABI of include/hyobfs.h.
+//
+// A context mirrors salamanderObfuscator (extras/obfs/salamander.go:26-32):
+// the PSK (here also its BLAKE2b prefix state, KeyParams), the salt source
+// (RandSrc), and a lock for the per-packet path (lk).  It is bound to one
+// HIP device.  Every compute call runs the gfx950 kernels of salamander.hip;
+// there is no CPU path.
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <new>
+#include <vector>
+
+#include "../../include/hyobfs.h"
+#include "kernels.h"
+
+using hyobfs::BatchParams;
+using hyobfs::KeyParams;
+
+struct hyobfs_salamander {
+    std::vector<uint8_t> psk;
+    int device = 0;
+    KeyParams kp{};
+    hipStream_t stream = nullptr;
+    std::mutex mu;              // per-packet path, salt source, owned buffers (lk)
+    uint64_t rng = 0;           // SplitMix64 state (RandSrc)
+    // per-packet staging in mapped pinned host memory: [in | out | salt | len | total]
+    uint8_t* stage = nullptr;
+    uint8_t* stage_dev = nullptr;
+    size_t stage_cap = 0;       // bytes for each of in and out
+    // context-owned batch workspace
+    void* ws = nullptr;
+    uint64_t ws_cap = 0;
+};
+
+namespace {
+
+struct DeviceGuard {   // keep the caller's current device unchanged
+    int prev = -1;
+    bool ok = false;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        ok = hipSetDevice(dev) == hipSuccess;
+    }
+    ~DeviceGuard() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
+
+// ---- BLAKE2b compression on the host, used only for the PSK-only prefix
+// blocks (blocks that hold no salt byte) when len(PSK) > 120.
+const uint64_t kIV[8] = {0x6a09e667f3bcc908ull, 0xbb67ae8584caa73bull, 0x3c6ef372fe94f82bull,
+                         0xa54ff53a5f1d36f1ull, 0x510e527fade682d1ull, 0x9b05688c2b3e6c1full,
+                         0x1f83d9abfb41bd6bull, 0x5be0cd19137e2179ull};
+const uint8_t kSigma[12][16] = {
+    {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15},
+    {14, 10, 4, 8, 9, 15, 13, 6, 1, 12, 0, 2, 11, 7, 5, 3},
+    {11, 8, 12, 0, 5, 2, 15, 13, 10, 14, 3, 6, 7, 1, 9, 4},
+    {7, 9, 3, 1, 13, 12, 11, 14, 2, 6, 5, 10, 4, 0, 15, 8},
+    {9, 0, 5, 7, 2, 4, 10, 15, 14, 1, 11, 12, 6, 8, 3, 13},
+    {2, 12, 6, 10, 0, 11, 8, 3, 4, 13, 7, 5, 15, 14, 1, 9},
+    {12, 5, 1, 15, 14, 13, 4, 10, 0, 7, 6, 3, 9, 2, 8, 11},
+    {13, 11, 7, 14, 12, 1, 3, 9, 5, 0, 15, 4, 8, 6, 2, 10},
+    {6, 15, 14, 9, 11, 3, 0, 8, 12, 2, 13, 7, 1, 4, 10, 5},
+    {10, 2, 8, 4, 7, 6, 1, 5, 15, 11, 9, 14, 3, 12, 13, 0},
+    {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15},
+    {14, 10, 4, 8, 9, 15, 13, 6, 1, 12, 0, 2, 11, 7, 5, 3}};
+
+inline uint64_t rotr(uint64_t x, int n) { return (x >> n) | (x << (64 - n)); }
+
+void host_compress(uint64_t h[8], const uint64_t m[16], uint64_t t, bool last) {
+    uint64_t v[16];
+    for (int i = 0; i < 8; ++i) {
+        v[i] = h[i];
+        v[i + 8] = kIV[i];
+    }
+    v[12] ^= t;
+    if (last) v[14] = ~v[14];
+    auto G = [&](int a, int b, int c, int d, uint64_t x, uint64_t y) {
+        v[a] = v[a] + v[b] + x;
+        v[d] = rotr(v[d] ^ v[a], 32);
+        v[c] = v[c] + v[d];
+        v[b] = rotr(v[b] ^ v[c], 24);
+        v[a] = v[a] + v[b] + y;
+        v[d] = rotr(v[d] ^ v[a], 16);
+        v[c] = v[c] + v[d];
+        v[b] = rotr(v[b] ^ v[c], 63);
+    };
+    for (int r = 0; r < 12; ++r) {
+        const uint8_t* s = kSigma[r];
+        G(0, 4, 8, 12, m[s[0]], m[s[1]]);
+        G(1, 5, 9, 13, m[s[2]], m[s[3]]);
+        G(2, 6, 10, 14, m[s[4]], m[s[5]]);
+        G(3, 7, 11, 15, m[s[6]], m[s[7]]);
+        G(0, 5, 10, 15, m[s[8]], m[s[9]]);
+        G(1, 6, 11, 12, m[s[10]], m[s[11]]);
+        G(2, 7, 8, 13, m[s[12]], m[s[13]]);
+        G(3, 4, 9, 14, m[s[14]], m[s[15]]);
+    }
+    for (int i = 0; i < 8; ++i) h[i] ^= v[i] ^ v[i + 8];
+}
+
+void block_words(const uint8_t* msg, size_t msg_len, size_t blk, uint64_t m[16]) {
+    for (int j = 0; j < 16; ++j) {
+        uint64_t w = 0;
+        for (int b = 7; b >= 0; --b) {
+            const size_t pos = 128 * blk + 8 * j + b;
+            w = (w << 8) | (pos < msg_len ? msg[pos] : 0u);
+        }
+        m[j] = w;
+    }
+}
+
+// keyLocked's hash, BLAKE2b-256(PSK || salt), split at the first block that
+// holds a salt byte: host compresses the blocks before it, the GPU the rest.
+KeyParams make_key_params(const uint8_t* psk, size_t psk_len) {
+    KeyParams k{};
+    const size_t T = psk_len + HYOBFS_SALT_LEN;
+    const size_t nb = (T + 127) / 128;                  // T >= 12, so nb >= 1
+    const size_t fb = psk_len / 128;                   // block with salt[0]
+    std::vector<uint8_t> msg(T, 0);                     // salt bytes stay 0
+    if (psk_len) std::memcpy(msg.data(), psk, psk_len);
+    for (int i = 0; i < 8; ++i) k.h[i] = kIV[i];
+    k.h[0] ^= 0x01010000ull ^ (uint64_t)HYOBFS_KEY_LEN;  // digest 32, unkeyed
+    for (size_t b = 0; b < fb; ++b) {                   // PSK-only blocks
+        uint64_t m[16];
+        block_words(msg.data(), T, b, m);
+        host_compress(k.h, m, 128ull * (b + 1), false);
+    }
+    k.nblk = (uint32_t)(nb - fb);                       // 1 or 2
+    for (uint32_t b = 0; b < k.nblk; ++b) {
+        block_words(msg.data(), T, fb + b, k.m + 16 * b);
+        k.t[b] = (fb + b + 1 == nb) ? (uint64_t)T : 128ull * (fb + b + 1);
+    }
+    k.salt_pos = (uint32_t)(psk_len - 128 * fb);
+    return k;
+}
+
+inline uint64_t splitmix_next(uint64_t& s) {
+    uint64_t z = (s += 0x9e3779b97f4a7c15ull);
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+    return z ^ (z >> 31);
+}
+
+bool is_gfx950(int dev) {
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return false;
+    return std::strncmp(prop.gcnArchName, "gfx950", 6) == 0;
+}
+
+// Ensure the mapped staging buffer holds `bytes` of input and of output.
+int ensure_stage(hyobfs_salamander* c, size_t bytes) {
+    if (bytes <= c->stage_cap && c->stage) return HYOBFS_OK;
+    size_t cap = c->stage_cap ? c->stage_cap : 4096;
+    while (cap < bytes) cap *= 2;
+    if (c->stage) (void)hipHostFree(c->stage);
+    c->stage = nullptr;
+    c->stage_cap = 0;
+    void* p = nullptr;
+    if (hipHostMalloc(&p, 2 * cap + 64, hipHostMallocMapped) != hipSuccess) return HYOBFS_ERR_NOMEM;
+    void* d = nullptr;
+    if (hipHostGetDevicePointer(&d, p, 0) != hipSuccess) {
+        (void)hipHostFree(p);
+        return HYOBFS_ERR_HIP;
+    }
+    c->stage = static_cast<uint8_t*>(p);
+    c->stage_dev = static_cast<uint8_t*>(d);
+    c->stage_cap = cap;
+    return HYOBFS_OK;
+}
+
+// One datagram through the batch kernel, staged in mapped pinned memory.
+// Caller holds c->mu and has checked the reference's length rules.
+size_t run_one(hyobfs_salamander* c, bool obf, const uint8_t* in, size_t in_len,
+               const uint8_t* salt, uint8_t* out, size_t W) {
+    DeviceGuard g(c->device);
+    if (!g.ok) return 0;
+    const size_t need = in_len > W ? in_len : W;
+    if (ensure_stage(c, need + 16) != HYOBFS_OK) return 0;
+    // layout: in at 0, out at cap (16-aligned), salt + len words at 2*cap
+    uint8_t* h_in = c->stage;
+    uint8_t* h_out = c->stage + c->stage_cap;
+    uint8_t* h_misc = c->stage + 2 * c->stage_cap;
+    if (in_len) std::memcpy(h_in, in, in_len);
+    if (obf) std::memcpy(h_misc, salt, HYOBFS_SALT_LEN);
+    uint32_t* h_len = reinterpret_cast<uint32_t*>(h_misc + 8);
+    *h_len = 0xFFFFFFFFu;
+    BatchParams b{};
+    b.n = 1;
+    b.in = c->stage_dev;
+    b.len_uniform = (uint32_t)in_len;
+    b.salts = reinterpret_cast<const uint64_t*>(c->stage_dev + 2 * c->stage_cap);
+    b.out = c->stage_dev + c->stage_cap;
+    b.out_cap = W;
+    b.out_stride = W;   // one slot of exactly len(out) = W bytes
+    b.pkt_cap = (uint32_t)W;
+    b.out_len = reinterpret_cast<uint32_t*>(c->stage_dev + 2 * c->stage_cap + 8);
+    if (hyobfs::launch_salamander(obf, b, c->kp, c->stream) != hipSuccess) return 0;
+    if (hipStreamSynchronize(c->stream) != hipSuccess) return 0;
+    if (*h_len != W) return 0;
+    std::memcpy(out, h_out, W);
+    return W;
+}
+
+int validate_and_fill(hyobfs_salamander* c, const hyobfs_batch* b, bool obf, BatchParams& bp,
+                      hipStream_t s) {
+    if (!c || !b) return HYOBFS_ERR_INVALID;
+    if (b->n && (!b->in || !b->out)) return HYOBFS_ERR_INVALID;
+    if (obf && b->n && !b->salts) return HYOBFS_ERR_INVALID;
+    if (reinterpret_cast<uintptr_t>(b->out) & 15) return HYOBFS_ERR_INVALID;
+    if (b->out_stride > hyobfs::kMaxDatagram) return HYOBFS_ERR_INVALID;
+    bp = BatchParams{};
+    bp.n = b->n;
+    bp.in = b->in;
+    bp.in_off = b->in_off;
+    bp.in_stride = b->in_stride;
+    bp.in_len = b->in_len;
+    bp.len_uniform = b->len_uniform;
+    uint64_t cap = b->pkt_cap ? b->pkt_cap : 0;
+    if (b->out_stride && (cap == 0 || b->out_stride < cap)) cap = b->out_stride;
+    bp.pkt_cap = (uint32_t)cap;
+    bp.salts = b->salts;
+    bp.out = b->out;
+    bp.out_cap = b->out_cap;
+    bp.out_stride = b->out_stride;
+    bp.out_off = b->out_off;
+    bp.out_len = b->out_len;
+    bp.out_total = reinterpret_cast<unsigned long long*>(b->out_total);
+    if (b->out_total && hipMemsetAsync(b->out_total, 0, sizeof(uint64_t), s) != hipSuccess)
+        return HYOBFS_ERR_HIP;
+    if (b->n && b->out_stride == 0) {   // packed: tile-sum scratch
+        const uint64_t need = hyobfs_batch_workspace_size(b->n);
+        if (b->workspace) {
+            if (b->workspace_bytes < need) return HYOBFS_ERR_INVALID;
+            bp.tile_sums = static_cast<uint64_t*>(b->workspace);
+        } else {
+            std::lock_guard<std::mutex> lk(c->mu);
+            if (c->ws_cap < need) {
+                if (c->ws) {
+                    (void)hipStreamSynchronize(s);
+                    (void)hipFree(c->ws);
+                }
+                c->ws = nullptr;
+                c->ws_cap = 0;
+                if (hipMalloc(&c->ws, need) != hipSuccess) return HYOBFS_ERR_NOMEM;
+                c->ws_cap = need;
+            }
+            bp.tile_sums = static_cast<uint64_t*>(c->ws);
+        }
+    }
+    return HYOBFS_OK;
+}
+
+int run_batch(hyobfs_salamander* c, const hyobfs_batch* b, void* stream, bool obf) {
+    if (!c || !b) return HYOBFS_ERR_INVALID;
+    DeviceGuard g(c->device);
+    if (!g.ok) return HYOBFS_ERR_HIP;
+    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : c->stream;
+    BatchParams bp;
+    const int rc = validate_and_fill(c, b, obf, bp, s);
+    if (rc != HYOBFS_OK) return rc;
+    return hyobfs::launch_salamander(obf, bp, c->kp, s) == hipSuccess ? HYOBFS_OK : HYOBFS_ERR_HIP;
+}
+
+}  // namespace
+
+extern "C" {
+
+int hyobfs_abi_version(void) { return HYOBFS_ABI_VERSION; }
+
+const char* hyobfs_status_string(int st) {
+    switch (st) {
+        case HYOBFS_OK: return "ok";
+        case HYOBFS_ERR_PSK_TOO_SHORT: return "PSK must be at least 4 bytes";
+        case HYOBFS_ERR_INVALID: return "invalid argument";
+        case HYOBFS_ERR_HIP: return "HIP runtime error";
+        case HYOBFS_ERR_NOMEM: return "out of memory";
+        case HYOBFS_ERR_NO_DEVICE: return "no usable gfx950 device";
+        case HYOBFS_ERR_IO: return "socket I/O error";
+        default: return "unknown status";
+    }
+}
+
+int hyobfs_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+int hyobfs_salamander_new(const uint8_t* psk, size_t psk_len, int device, hyobfs_salamander** out) {
+    if (!out) return HYOBFS_ERR_INVALID;
+    if (psk_len < HYOBFS_PSK_MIN_LEN) return HYOBFS_ERR_PSK_TOO_SHORT;   // salamander.go:35-37
+    if (!psk) return HYOBFS_ERR_INVALID;
+    if (device < 0 || device >= hyobfs_device_count() || !is_gfx950(device)) return HYOBFS_ERR_NO_DEVICE;
+    auto* c = new (std::nothrow) hyobfs_salamander();
+    if (!c) return HYOBFS_ERR_NOMEM;
+    c->psk.assign(psk, psk + psk_len);                                  // pskCopy, :38
+    c->device = device;
+    c->kp = make_key_params(psk, psk_len);
+    c->rng = (uint64_t)std::chrono::high_resolution_clock::now().time_since_epoch().count();  // :43
+    {
+        DeviceGuard g(device);
+        if (!g.ok || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+            delete c;
+            return HYOBFS_ERR_HIP;
+        }
+    }
+    *out = c;
+    return HYOBFS_OK;
+}
+
+void hyobfs_salamander_free(hyobfs_salamander* c) {
+    if (!c) return;
+    {
+        DeviceGuard g(c->device);
+        if (c->stream) {
+            (void)hipStreamSynchronize(c->stream);
+            (void)hipStreamDestroy(c->stream);
+        }
+        if (c->ws) (void)hipFree(c->ws);
+        if (c->stage) (void)hipHostFree(c->stage);
+    }
+    delete c;
+}
+
+int hyobfs_salamander_device(const hyobfs_salamander* c) { return c ? c->device : -1; }
+
+void hyobfs_salamander_seed(hyobfs_salamander* c, uint64_t seed) {
+    if (!c) return;
+    std::lock_guard<std::mutex> lk(c->mu);
+    c->rng = seed;
+}
+
+void hyobfs_salamander_next_salts(hyobfs_salamander* c, uint8_t* salts, size_t n) {
+    if (!c || !salts) return;
+    std::lock_guard<std::mutex> lk(c->mu);
+    for (size_t i = 0; i < n; ++i) {
+        const uint64_t x = splitmix_next(c->rng);
+        std::memcpy(salts + 8 * i, &x, 8);   // little-endian host
+    }
+}
+
+int hyobfs_salamander_key(hyobfs_salamander* c, const uint8_t salt[8], uint8_t key[32]) {
+    if (!c || !salt || !key) return HYOBFS_ERR_INVALID;
+    std::lock_guard<std::mutex> lk(c->mu);
+    DeviceGuard g(c->device);
+    if (!g.ok) return HYOBFS_ERR_HIP;
+    if (ensure_stage(c, 64) != HYOBFS_OK) return HYOBFS_ERR_NOMEM;
+    std::memcpy(c->stage, salt, 8);
+    if (hyobfs::launch_keys(c->kp, reinterpret_cast<const uint64_t*>(c->stage_dev),
+                            c->stage_dev + c->stage_cap, 1, c->stream) != hipSuccess)
+        return HYOBFS_ERR_HIP;
+    if (hipStreamSynchronize(c->stream) != hipSuccess) return HYOBFS_ERR_HIP;
+    std::memcpy(key, c->stage + c->stage_cap, 32);
+    return HYOBFS_OK;
+}
+
+int hyobfs_salamander_keys_batch(hyobfs_salamander* c, const uint64_t* salts, uint8_t* keys,
+                                 uint64_t n, void* stream) {
+    if (!c || (n && (!salts || !keys))) return HYOBFS_ERR_INVALID;
+    DeviceGuard g(c->device);
+    if (!g.ok) return HYOBFS_ERR_HIP;
+    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : c->stream;
+    return hyobfs::launch_keys(c->kp, salts, keys, n, s) == hipSuccess ? HYOBFS_OK : HYOBFS_ERR_HIP;
+}
+
+size_t hyobfs_salamander_obfuscate(hyobfs_salamander* c, const uint8_t* in, size_t in_len,
+                                   const uint8_t salt[8], uint8_t* out, size_t out_len) {
+    if (!c || !salt || (!in && in_len)) return 0;
+    const size_t W = in_len + HYOBFS_SALT_LEN;
+    if (out_len < W || !out) return 0;                         // salamander.go:60-62
+    if (in_len > hyobfs::kMaxDatagram) return 0;
+    std::lock_guard<std::mutex> lk(c->mu);
+    return run_one(c, true, in, in_len, salt, out, W);
+}
+
+size_t hyobfs_salamander_obfuscate_auto(hyobfs_salamander* c, const uint8_t* in, size_t in_len,
+                                        uint8_t* out, size_t out_len) {
+    if (!c || (!in && in_len)) return 0;
+    const size_t W = in_len + HYOBFS_SALT_LEN;
+    if (out_len < W || !out) return 0;                         // salamander.go:60-62
+    if (in_len > hyobfs::kMaxDatagram) return 0;
+    std::lock_guard<std::mutex> lk(c->mu);
+    uint8_t salt[8];
+    const uint64_t x = splitmix_next(c->rng);                   // RandSrc.Read, :65
+    std::memcpy(salt, &x, 8);
+    return run_one(c, true, in, in_len, salt, out, W);
+}
+
+size_t hyobfs_salamander_deobfuscate(hyobfs_salamander* c, const uint8_t* in, size_t in_len,
+                                     uint8_t* out, size_t out_len) {
+    if (!c || (!in && in_len)) return 0;
+    if (in_len <= HYOBFS_SALT_LEN) return 0;                   // salamander.go:75-76
+    const size_t W = in_len - HYOBFS_SALT_LEN;
+    if (out_len < W || !out) return 0;                         // :76-77
+    if (in_len > hyobfs::kMaxDatagram) return 0;
+    std::lock_guard<std::mutex> lk(c->mu);
+    return run_one(c, false, in, in_len, nullptr, out, W);
+}
+
+uint64_t hyobfs_batch_workspace_size(uint64_t n) {
+    const uint64_t ntiles = (n + hyobfs::kTile - 1) / hyobfs::kTile;
+    return (ntiles + 1) * sizeof(uint64_t);
+}
+
+int hyobfs_salamander_obfuscate_batch(hyobfs_salamander* c, const hyobfs_batch* b, void* stream) {
+    return run_batch(c, b, stream, true);
+}
+
+int hyobfs_salamander_deobfuscate_batch(hyobfs_salamander* c, const hyobfs_batch* b, void* stream) {
+    return run_batch(c, b, stream, false);
+}
+
+int hyobfs_synth_stream(uint8_t* dst, uint64_t nbytes, uint64_t seed, uint64_t start, void* stream) {
+    if (!dst || (reinterpret_cast<uintptr_t>(dst) & 15)) return HYOBFS_ERR_INVALID;
+    return hyobfs::launch_synth_stream(dst, nbytes, seed, start, static_cast<hipStream_t>(stream)) ==
+                   hipSuccess
+               ? HYOBFS_OK
+               : HYOBFS_ERR_HIP;
+}
+
+int hyobfs_synth_u64(uint64_t* dst, uint64_t n, uint64_t seed, uint64_t first, void* stream) {
+    if (!dst) return HYOBFS_ERR_INVALID;
+    return hyobfs::launch_synth_u64(dst, n, seed, first, static_cast<hipStream_t>(stream)) == hipSuccess
+               ? HYOBFS_OK
+               : HYOBFS_ERR_HIP;
+}
+
+int hyobfs_synth_bimodal_lengths(uint32_t* dst, uint64_t n, uint64_t seed, uint64_t first,
+                                 void* stream) {
+    if (!dst) return HYOBFS_ERR_INVALID;
+    return hyobfs::launch_synth_bimodal(dst, n, seed, first, static_cast<hipStream_t>(stream)) ==
+                   hipSuccess
+               ? HYOBFS_OK
+               : HYOBFS_ERR_HIP;
+}
+
+}  // extern "C"

@@ -1,0 +1,57 @@
+// Private interface between the C ABI layer (hyobfs_api.cpp) and the gfx950
+// kernels (salamander.hip).  Not installed; include/hyobfs.h is the ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace hyobfs {
+
+constexpr int kTile = 256;          // datagrams per workgroup tile (= threads)
+constexpr uint32_t kMaxDatagram = (1u << 24) - 64;  // longest datagram a batch accepts
+constexpr uint64_t kMaxStride = 1ull << 24;         // longest slot of a slotted output
+
+// BLAKE2b state for the per-packet key, precomputed on the host from the PSK
+// alone (salamander.go:88-91 hashes PSK || salt; every block before the one
+// holding salt[0] depends on the PSK only).  The device compresses the last
+// one or two blocks, which carry the salt.
+struct KeyParams {
+    uint64_t h[8];       // chaining value entering the first device block
+    uint64_t m[32];      // message words of the device blocks, salt bytes = 0
+    uint64_t t[2];       // byte counter after each device block
+    uint32_t nblk;       // 1 or 2 device blocks
+    uint32_t salt_pos;   // byte offset of salt[0] in the device blocks (0..127)
+};
+
+// One batch launch (include/hyobfs.h, struct hyobfs_batch, plus derived values).
+struct BatchParams {
+    uint64_t n;
+    const uint8_t* in;
+    const uint64_t* in_off;
+    uint64_t in_stride;
+    const uint32_t* in_len;
+    uint32_t len_uniform;
+    uint32_t pkt_cap;       // effective per-packet cap (slot and pkt_cap folded), 0 = none
+    const uint64_t* salts;
+    uint8_t* out;
+    uint64_t out_cap;
+    uint64_t out_stride;    // 0 = packed
+    double inv_stride;      // 1.0 / out_stride (slotted chunk -> packet lookup)
+    uint64_t* out_off;
+    uint32_t* out_len;
+    unsigned long long* out_total;
+    const uint64_t* tile_prefix;  // packed: exclusive prefix of tile sums (ntiles+1)
+    uint64_t* tile_sums;          // packed: scratch, ntiles+1 entries
+};
+
+hipError_t launch_salamander(bool obfuscate, const BatchParams& b, const KeyParams& k,
+                             hipStream_t s);
+hipError_t launch_keys(const KeyParams& k, const uint64_t* salts, uint8_t* keys, uint64_t n,
+                       hipStream_t s);
+hipError_t launch_synth_stream(uint8_t* dst, uint64_t nbytes, uint64_t seed, uint64_t start,
+                               hipStream_t s);
+hipError_t launch_synth_u64(uint64_t* dst, uint64_t n, uint64_t seed, uint64_t first,
+                            hipStream_t s);
+hipError_t launch_synth_bimodal(uint32_t* dst, uint64_t n, uint64_t seed, uint64_t first,
+                                hipStream_t s);
+
+}  // namespace hyobfs

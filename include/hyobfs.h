@@ -1,0 +1,187 @@
+/*
+ * hyobfs.h -- C ABI of libhyobfs: Hysteria "Salamander" packet obfuscation on
+ * AMD Instinct MI355X (gfx950).
+ *
+ * The ABI replaces, one for one, the Go surface of the reference's hot path
+ * (paths relative to apernet/hysteria):
+ *
+ *   Go (reference)                                       C ABI (this header)
+ *   ---------------------------------------------------  -----------------------------------
+ *   newSalamanderObfuscator(psk)  extras/obfs/salamander.go:34-46
+ *                                                        hyobfs_salamander_new
+ *   ErrPSKTooShort                extras/obfs/salamander.go:21
+ *                                                        HYOBFS_ERR_PSK_TOO_SHORT
+ *   (o *salamanderObfuscator).Obfuscate(in, out) int     salamander.go:59-72
+ *                                                        hyobfs_salamander_obfuscate
+ *   (o *salamanderObfuscator).Deobfuscate(in, out) int   salamander.go:74-86
+ *                                                        hyobfs_salamander_deobfuscate
+ *   keyLocked(salt) [32]byte      salamander.go:88-91    hyobfs_salamander_key
+ *   obfuscator interface          extras/obfs/conn.go:15-18
+ *                                                        the two calls above (per datagram)
+ *                                                        + the *_batch calls (N datagrams)
+ *   RandSrc (math/rand, :29,43,65) salt source           hyobfs_salamander_seed / _next_salts
+ *   obfsPacketConn.ReadFrom/WriteTo  extras/obfs/conn.go:73-99
+ *                                                        include/hyobfs_conn.h
+ *
+ * Rules kept from the reference:
+ *   - A per-packet call returns the number of bytes written to out, and 0 for
+ *     an invalid packet or a too-small out buffer (conn.go:12-14).  There is no
+ *     per-packet error value.
+ *   - Obfuscate writes len(in)+8 bytes: the 8-byte salt, then in[i] ^ key[i%32];
+ *     it returns 0 when out_len < in_len + 8 (salamander.go:60-62).
+ *   - Deobfuscate writes len(in)-8 bytes and returns 0 when in_len <= 8 or
+ *     out_len < in_len - 8 (salamander.go:75-77).
+ *   - key = BLAKE2b-256(PSK || salt), unkeyed (salamander.go:88-91).
+ *   - Construction fails with HYOBFS_ERR_PSK_TOO_SHORT for PSK < 4 bytes.
+ *
+ * The salt: the reference draws it from a time-seeded math/rand source inside
+ * Obfuscate (salamander.go:43,65).  Here the caller passes it (a Go adapter
+ * reads its own RandSrc under its lock, so wire bytes stay identical), or asks
+ * the context's generator for it (hyobfs_salamander_next_salts).
+ *
+ * Threading: a context may be used from several threads.  The per-packet
+ * calls serialise on the context (like the reference's lk, salamander.go:64-67);
+ * batch calls only enqueue work on the caller's stream.
+ *
+ * Every compute call runs on the GPU.  There is no CPU fallback: without a
+ * usable gfx950 device hyobfs_salamander_new fails with HYOBFS_ERR_NO_DEVICE.
+ */
+#ifndef HYOBFS_H
+#define HYOBFS_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HYOBFS_ABI_VERSION 1
+
+#define HYOBFS_PSK_MIN_LEN 4  /* smPSKMinLen, salamander.go:14 */
+#define HYOBFS_SALT_LEN 8     /* smSaltLen,   salamander.go:15 */
+#define HYOBFS_KEY_LEN 32     /* smKeyLen,    salamander.go:16 */
+#define HYOBFS_UDP_BUFFER_SIZE 2048 /* udpBufferSize, conn.go:10 */
+
+/* status codes (negative = error) */
+#define HYOBFS_OK 0
+#define HYOBFS_ERR_PSK_TOO_SHORT (-1) /* ErrPSKTooShort, salamander.go:21 */
+#define HYOBFS_ERR_INVALID (-2)       /* bad argument (NULL, misaligned, ...) */
+#define HYOBFS_ERR_HIP (-3)           /* HIP runtime error */
+#define HYOBFS_ERR_NOMEM (-4)         /* allocation failed */
+#define HYOBFS_ERR_NO_DEVICE (-5)     /* no usable gfx950 device */
+#define HYOBFS_ERR_IO (-6)            /* socket error (hyobfs_conn_*); errno kept */
+
+typedef struct hyobfs_salamander hyobfs_salamander; /* opaque context */
+
+/* ------------------------------------------------------------------ basics */
+int hyobfs_abi_version(void);
+const char* hyobfs_status_string(int status);
+/* number of HIP devices visible to this process (0 when none) */
+int hyobfs_device_count(void);
+
+/* ------------------------------------------------------------- lifecycle */
+/* newSalamanderObfuscator (salamander.go:34-46) + GPU binding.  Copies the
+   PSK, precomputes its BLAKE2b prefix, binds the context to HIP device
+   `device`.  *out is set only on HYOBFS_OK. */
+int hyobfs_salamander_new(const uint8_t* psk, size_t psk_len, int device,
+                          hyobfs_salamander** out);
+void hyobfs_salamander_free(hyobfs_salamander* ctx);
+int hyobfs_salamander_device(const hyobfs_salamander* ctx);
+
+/* Salt source (the reference's RandSrc, salamander.go:29,43,65).  The context
+   seeds itself from the clock at creation like the reference; _seed makes it
+   deterministic.  _next_salts writes n salts (8 bytes each, in host memory). */
+void hyobfs_salamander_seed(hyobfs_salamander* ctx, uint64_t seed);
+void hyobfs_salamander_next_salts(hyobfs_salamander* ctx, uint8_t* salts, size_t n);
+
+/* ---------------------------------------------------------- per datagram */
+/* keyLocked (salamander.go:88-91) computed on the GPU: key = BLAKE2b-256(PSK||salt). */
+int hyobfs_salamander_key(hyobfs_salamander* ctx, const uint8_t salt[8],
+                          uint8_t key[32]);
+/* keyLocked for n salts at once: keys[32*i..] = BLAKE2b-256(PSK || salts[i]).
+   Device pointers, enqueued on stream (NULL = the context's stream). */
+int hyobfs_salamander_keys_batch(hyobfs_salamander* ctx, const uint64_t* salts,
+                                 uint8_t* keys, uint64_t n, void* stream);
+/* Obfuscate (salamander.go:59-72) with an explicit salt.  Host buffers, synchronous. */
+size_t hyobfs_salamander_obfuscate(hyobfs_salamander* ctx, const uint8_t* in,
+                                   size_t in_len, const uint8_t salt[8],
+                                   uint8_t* out, size_t out_len);
+/* Obfuscate drawing the salt from the context's generator (the exact
+   reference call shape: Obfuscate(in, out) int). */
+size_t hyobfs_salamander_obfuscate_auto(hyobfs_salamander* ctx, const uint8_t* in,
+                                        size_t in_len, uint8_t* out, size_t out_len);
+/* Deobfuscate (salamander.go:74-86).  Host buffers, synchronous. */
+size_t hyobfs_salamander_deobfuscate(hyobfs_salamander* ctx, const uint8_t* in,
+                                     size_t in_len, uint8_t* out, size_t out_len);
+
+/* ------------------------------------------------------------------ batch */
+/*
+ * A batch of n datagrams in device-accessible memory (device memory, or
+ * mapped pinned host memory).  Per packet i:
+ *
+ *   input   : len  L_i = in_len ? in_len[i] : len_uniform
+ *             bytes at in + (in_off ? in_off[i] : i * in_stride)       (any alignment)
+ *   salt    : obfuscate only: salts[i], 8 bytes, little-endian u64
+ *             (salt byte b = (salts[i] >> 8b) & 0xff)
+ *   output  : W_i = L_i + 8 (obfuscate) or L_i - 8 (deobfuscate)
+ *             valid iff W_i > 0 and W_i <= cap_i, where cap_i = pkt_cap
+ *             (0 = unlimited), further limited to out_stride when slotted
+ *             (that is `len(out)` of the per-packet call)
+ *   layout  : out_stride > 0  -> slotted: out_off_i = i * out_stride
+ *             out_stride == 0 -> packed : out_off_i = exclusive prefix sum of
+ *                                the valid W's (the datagrams sit back to back)
+ *             a packet whose region passes out_cap is dropped (packed: so is
+ *             every later one, offsets never move)
+ *   result  : out_off[i] (if non-NULL) = out_off_i; out_len[i] (if non-NULL)
+ *             = W_i, or 0 for a dropped packet (the reference's "return 0");
+ *             *out_total (if non-NULL, device memory) = bytes written.
+ *             Bytes of `out` outside valid regions are not written.
+ *
+ * `out` must be 16-byte aligned.  All pointers are device-accessible; the
+ * call only enqueues work on `stream` (a hipStream_t; NULL = the context's
+ * own stream) and returns.  workspace: device scratch of at least
+ * hyobfs_batch_workspace_size(n) bytes, or NULL to use a context-owned buffer
+ * (then the first call of a new maximum size allocates and is not
+ * graph-capturable).
+ */
+typedef struct hyobfs_batch {
+    uint64_t n;
+    const uint8_t* in;
+    const uint64_t* in_off;
+    uint64_t in_stride;
+    const uint32_t* in_len;
+    uint32_t len_uniform;
+    uint32_t pkt_cap;
+    const uint64_t* salts;
+    uint8_t* out;
+    uint64_t out_cap;
+    uint64_t out_stride;
+    uint64_t* out_off;
+    uint32_t* out_len;
+    uint64_t* out_total;
+    void* workspace;
+    uint64_t workspace_bytes;
+} hyobfs_batch;
+
+uint64_t hyobfs_batch_workspace_size(uint64_t n);
+int hyobfs_salamander_obfuscate_batch(hyobfs_salamander* ctx, const hyobfs_batch* b,
+                                      void* stream);
+int hyobfs_salamander_deobfuscate_batch(hyobfs_salamander* ctx, const hyobfs_batch* b,
+                                        void* stream);
+
+/* ----------------------------------------------- synthetic inputs (bench) */
+/* Device-side generators of the seeded inputs of BASELINE.md ("Synthetic
+   inputs"), so large batches never cross PCIe.  SplitMix64 counter form:
+   x_k = mix(seed + (k+1) * 0x9e3779b97f4a7c15). */
+int hyobfs_synth_stream(uint8_t* dst, uint64_t nbytes, uint64_t seed,
+                        uint64_t start_byte, void* stream);
+int hyobfs_synth_u64(uint64_t* dst, uint64_t n, uint64_t seed, uint64_t first,
+                     void* stream);
+int hyobfs_synth_bimodal_lengths(uint32_t* dst, uint64_t n, uint64_t seed,
+                                 uint64_t first, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HYOBFS_H */

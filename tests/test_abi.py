@@ -1,0 +1,65 @@
+"""CPU tests of the drop-in boundary: libhyobfs.so loads, exports every symbol
+declared in include/*.h, and its struct layout matches the header (checked
+by compiling a probe against the header with gcc).  No compute without a GPU."""
+import ctypes
+import os
+import subprocess
+
+import pytest
+
+from hysteria_amd import _lib
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_library_exports_every_header_symbol():
+    lib = _lib.load()
+    names = _lib.header_functions()
+    assert len(names) >= 15
+    missing = [n for n in names if not hasattr(lib, n)]
+    assert not missing, missing
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True,
+                         check=True).stdout
+    exported = {ln.split()[-1] for ln in out.splitlines() if " T " in ln}
+    assert set(names) <= exported
+
+
+def test_abi_basics():
+    lib = _lib.load()
+    assert lib.hyobfs_abi_version() == 1
+    assert _lib.status_string(_lib.HYOBFS_ERR_PSK_TOO_SHORT) == "PSK must be at least 4 bytes"
+    assert lib.hyobfs_batch_workspace_size(0) == 8
+    assert lib.hyobfs_batch_workspace_size(257) == 3 * 8
+
+
+def test_psk_too_short_before_device_check():
+    """ErrPSKTooShort comes from the constructor (salamander.go:35-37) on any machine."""
+    import hysteria_amd
+    with pytest.raises(hysteria_amd.PSKTooShortError):
+        hysteria_amd.SalamanderObfuscator(b"abc")
+
+
+def test_no_cpu_fallback_without_gpu():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    import hysteria_amd
+    with pytest.raises(_lib.HyobfsError) as e:
+        hysteria_amd.SalamanderObfuscator(b"average_password")
+    assert e.value.status == _lib.HYOBFS_ERR_NO_DEVICE
+
+
+def test_batch_struct_layout_matches_header(tmp_path):
+    fields = [f[0] for f in _lib.HyobfsBatch._fields_]
+    cnames = ["n", "in", "in_off", "in_stride", "in_len", "len_uniform", "pkt_cap", "salts", "out",
+              "out_cap", "out_stride", "out_off", "out_len", "out_total", "workspace", "workspace_bytes"]
+    assert len(fields) == len(cnames)
+    src = tmp_path / "probe.c"
+    body = "\n".join(f'printf("%zu\\n", offsetof(hyobfs_batch, {c}));' for c in cnames)
+    src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "hyobfs.h"\nint main(void){\n'
+                   + body + '\nprintf("%zu\\n", sizeof(hyobfs_batch));return 0;}\n')
+    exe = tmp_path / "probe"
+    subprocess.run(["gcc", "-std=c11", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
+    vals = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()]
+    py = [getattr(_lib.HyobfsBatch, f).offset for f in fields] + [ctypes.sizeof(_lib.HyobfsBatch)]
+    assert vals == py

@@ -1,0 +1,310 @@
+"""GPU parity: the gfx950 kernels (through the C ABI) against the oracle.
+
+Bit-exact everywhere (byte work).  Small and medium cases compare every byte
+with the C restatement and the golden fixtures; the BASELINE.json full sizes
+compare SHA-256 digests committed in tests/golden/batch_digests.json plus a
+device round trip (obfuscate -> deobfuscate == input).
+"""
+import hashlib
+
+import numpy as np
+import pytest
+
+from oracle import salamander_ref as ref
+
+pytestmark = pytest.mark.gpu
+
+PSK = b"average_password"
+
+
+@pytest.fixture(scope="module")
+def obfs(gpu):
+    import hysteria_amd
+    o = hysteria_amd.SalamanderObfuscator(PSK, 0)
+    yield o
+    o.close()
+
+
+def _dev(a, gpu):
+    import torch
+    return torch.from_numpy(np.ascontiguousarray(a)).to(gpu)
+
+
+def _u64(a, gpu):
+    import torch
+    return torch.from_numpy(np.ascontiguousarray(a).view(np.int64)).to(gpu)
+
+
+def _u32(a, gpu):
+    import torch
+    return torch.from_numpy(np.ascontiguousarray(a).view(np.int32)).to(gpu)
+
+
+def _host(t):
+    import torch
+    torch.cuda.synchronize()
+    return t.cpu().numpy()
+
+
+# ------------------------------------------------------------------ per packet
+def test_golden_vectors_per_packet(golden, gpu):
+    import hysteria_amd
+    ctxs = {}
+    try:
+        for v in golden[0]["vectors"]:
+            psk = bytes.fromhex(v["psk"])
+            if psk not in ctxs:
+                ctxs[psk] = hysteria_amd.SalamanderObfuscator(psk, 0)
+            o = ctxs[psk]
+            salt = bytes.fromhex(v["salt"])
+            payload = ref.stream_bytes(v["payload_seed"], v["payload_start"], v["payload_len"])
+            assert o.key(salt).hex() == v["key"]
+            out = bytearray(hysteria_amd.UDP_BUFFER_SIZE + 64)
+            n = o.obfuscate(payload, out, salt=salt)
+            assert n == len(payload) + 8
+            wire = bytes(out[:n])
+            assert hashlib.sha256(wire).hexdigest() == v["wire_sha256"]
+            if "wire" in v:
+                assert wire.hex() == v["wire"]
+            back = bytearray(len(wire))
+            m = o.deobfuscate(wire, back)
+            if payload:
+                assert m == len(payload) and bytes(back[:m]) == payload
+            else:
+                assert m == 0
+    finally:
+        for o in ctxs.values():
+            o.close()
+
+
+def test_edge_rules_per_packet(obfs):
+    salt = b"\x01" * 8
+    assert obfs.obfuscate(b"x" * 10, bytearray(17), salt=salt) == 0   # salamander.go:60-62
+    out = bytearray(18)
+    assert obfs.obfuscate(b"x" * 10, out, salt=salt) == 18
+    assert bytes(out) == ref.obfuscate(PSK, b"x" * 10, salt)
+    out = bytearray(8)
+    assert obfs.obfuscate(b"", out, salt=salt) == 8 and bytes(out) == salt
+    for n in (0, 1, 7, 8):                                           # :75-76
+        assert obfs.deobfuscate(b"\x00" * n, bytearray(2048)) == 0
+    assert obfs.deobfuscate(b"\x00" * 20, bytearray(11)) == 0         # :76-77
+    assert obfs.deobfuscate(b"\x00" * 20, bytearray(12)) == 12
+
+
+def test_reference_roundtrip_1000x1200_auto_salts(obfs):
+    """TestSalamanderObfuscator (salamander_test.go:32-45) on the GPU path."""
+    rng = np.random.default_rng(3)
+    o_out, d_out = bytearray(2048), bytearray(2048)
+    obfs.seed(12345)
+    for _ in range(1000):
+        payload = rng.integers(0, 256, 1200, dtype=np.uint8).tobytes()
+        n = obfs.obfuscate(payload, o_out)
+        assert n == len(payload) + 8
+        m = obfs.deobfuscate(bytes(o_out[:n]), d_out)
+        assert m == len(payload) and bytes(d_out[:m]) == payload
+        assert bytes(o_out[:n]) == ref.obfuscate(PSK, payload, bytes(o_out[:8]))
+
+
+@pytest.mark.parametrize("psk_len", [4, 5, 16, 119, 120, 121, 124, 127, 128, 129, 200, 248, 249, 256, 300])
+def test_keys_batch_vs_hashlib(gpu, psk_len):
+    import hysteria_amd
+    import torch
+    psk = ref.stream_bytes(9, 0, psk_len)
+    n = 20000
+    salts = ref.splitmix64_array(17, 0, n)
+    with hysteria_amd.SalamanderObfuscator(psk, 0) as o:
+        keys = torch.empty(32 * n, dtype=torch.uint8, device=gpu)
+        o.keys_batch(_u64(salts, gpu), keys, n)
+        got = _host(keys).reshape(n, 32)
+    for i in range(0, n, 7):
+        assert got[i].tobytes() == ref.key(psk, int(salts[i]).to_bytes(8, "little")), i
+
+
+# ------------------------------------------------------------------ batches
+def _uniform_inputs(gpu, n, L, seed_payload=1, seed_salt=2):
+    import torch
+    import hysteria_amd
+    inp = torch.empty(max(n * L, 16), dtype=torch.uint8, device=gpu)
+    hysteria_amd.synth_stream(inp, n * L, seed_payload, 0)
+    salts = torch.empty(n, dtype=torch.int64, device=gpu)
+    hysteria_amd.synth_u64(salts, n, seed_salt, 0)
+    return inp, salts
+
+
+@pytest.mark.parametrize("n", [1, 2, 255, 256, 257, 1000, 65536])
+def test_uniform_1200_vs_oracle(obfs, gpu, coracle, n):
+    import torch
+    L = 1200
+    inp, salts = _uniform_inputs(gpu, n, L)
+    out = torch.empty(n * (L + 8), dtype=torch.uint8, device=gpu)
+    out_len = torch.empty(n, dtype=torch.int32, device=gpu)
+    total = torch.zeros(1, dtype=torch.int64, device=gpu)
+    obfs.obfuscate_batch(inp, n, in_stride=L, len_uniform=L, salts=salts, out=out, out_stride=L + 8,
+                         out_len=out_len, out_total=total)
+    h_in = _host(inp)[: n * L]
+    assert np.array_equal(h_in, coracle.fill_stream(1, 0, n * L))
+    exp, _, _, _ = coracle.batch(True, PSK, n, h_in, in_stride=L, len_uniform=L,
+                                 salts=coracle.salts(2, 0, n), out_cap=n * (L + 8))
+    got = _host(out)
+    assert np.array_equal(got, exp)
+    assert (_host(out_len) == L + 8).all()
+    assert int(_host(total)[0]) == n * (L + 8)
+    # deobfuscate back, packed output
+    back = torch.empty(n * L, dtype=torch.uint8, device=gpu)
+    obfs.deobfuscate_batch(out, n, in_stride=L + 8, len_uniform=L + 8, out=back)
+    assert np.array_equal(_host(back), h_in)
+
+
+def test_uniform_digest_64k_golden(obfs, gpu, golden):
+    import torch
+    d = golden[1]["small_64k_x_1200"]
+    n, L = d["n"], d["len"]
+    inp, salts = _uniform_inputs(gpu, n, L)
+    out = torch.empty(n * (L + 8), dtype=torch.uint8, device=gpu)
+    obfs.obfuscate_batch(inp, n, in_stride=L, len_uniform=L, salts=salts, out=out)   # packed layout
+    assert hashlib.sha256(_host(out).tobytes()).hexdigest() == d["obf_sha256"]
+
+
+def test_config2_1M_x_1200_digest_and_roundtrip(obfs, gpu, golden):
+    """BASELINE configs[1] at full size: digest + device round trip."""
+    import torch
+    d = golden[1]["config2_1M_x_1200"]
+    n, L = d["n"], d["len"]
+    inp, salts = _uniform_inputs(gpu, n, L)
+    out = torch.empty(n * (L + 8), dtype=torch.uint8, device=gpu)
+    obfs.obfuscate_batch(inp, n, in_stride=L, len_uniform=L, salts=salts, out=out, out_stride=L + 8)
+    assert hashlib.sha256(_host(out).tobytes()).hexdigest() == d["obf_sha256"]
+    back = torch.empty(n * L, dtype=torch.uint8, device=gpu)
+    obfs.deobfuscate_batch(out, n, in_stride=L + 8, len_uniform=L + 8, out=back, out_stride=L)
+    torch.cuda.synchronize()
+    assert torch.equal(back, inp[: n * L])
+
+
+def _bimodal(gpu, n):
+    import torch
+    import hysteria_amd
+    lens = torch.empty(n, dtype=torch.int32, device=gpu)
+    hysteria_amd.synth_bimodal_lengths(lens, n, 3, 0)
+    in_off = torch.zeros(n, dtype=torch.int64, device=gpu)
+    in_off[1:] = torch.cumsum(lens[:-1].to(torch.int64), 0)
+    total_in = int(lens.to(torch.int64).sum())
+    inp = torch.empty(total_in + 16, dtype=torch.uint8, device=gpu)
+    hysteria_amd.synth_stream(inp, total_in, 1, 0)
+    salts = torch.empty(n, dtype=torch.int64, device=gpu)
+    hysteria_amd.synth_u64(salts, n, 2, 0)
+    return lens, in_off, inp, salts, total_in
+
+
+def test_bimodal_64k_vs_oracle_and_digest(obfs, gpu, coracle, golden):
+    import torch
+    d = golden[1]["bimodal_64k"]
+    n = d["n"]
+    lens, in_off, inp, salts, total_in = _bimodal(gpu, n)
+    assert total_in == d["in_bytes"]
+    cap = total_in + 8 * n
+    out = torch.empty(cap, dtype=torch.uint8, device=gpu)
+    out_off = torch.empty(n, dtype=torch.int64, device=gpu)
+    out_len = torch.empty(n, dtype=torch.int32, device=gpu)
+    obfs.obfuscate_batch(inp, n, in_off=in_off, in_len=lens, salts=salts, out=out, out_cap=cap,
+                         out_off=out_off, out_len=out_len)
+    got = _host(out)
+    assert hashlib.sha256(got.tobytes()).hexdigest() == d["obf_sha256"]
+    h_lens = _host(lens).view(np.uint32)
+    exp, eoff, elen, _ = coracle.batch(True, PSK, n, _host(inp), in_off=_host(in_off).view(np.uint64),
+                                       in_len=h_lens, salts=coracle.salts(2, 0, n), out_cap=cap)
+    assert np.array_equal(got, exp)
+    assert np.array_equal(_host(out_off).view(np.uint64), eoff)
+    assert np.array_equal(_host(out_len).view(np.uint32), elen)
+    # deobfuscate the packed wire back
+    back = torch.empty(total_in + 16, dtype=torch.uint8, device=gpu)
+    wlen = out_len
+    obfs.deobfuscate_batch(out, n, in_off=out_off, in_len=wlen, out=back, out_cap=total_in)
+    assert np.array_equal(_host(back)[:total_in], _host(inp)[:total_in])
+
+
+def test_config3_bimodal_4M_digest(obfs, gpu, golden):
+    import torch
+    d = golden[1]["config3_bimodal_4M"]
+    n = d["n"]
+    lens, in_off, inp, salts, total_in = _bimodal(gpu, n)
+    assert total_in == d["in_bytes"]
+    cap = total_in + 8 * n
+    out = torch.empty(cap, dtype=torch.uint8, device=gpu)
+    obfs.obfuscate_batch(inp, n, in_off=in_off, in_len=lens, salts=salts, out=out, out_cap=cap)
+    h = hashlib.sha256()
+    torch.cuda.synchronize()
+    step = 1 << 28
+    for s in range(0, cap, step):
+        h.update(out[s:s + step].cpu().numpy().tobytes())
+    assert h.hexdigest() == d["obf_sha256"]
+
+
+def _ragged_case(seed, n, maxlen, gap_max, base_misalign):
+    rng = np.random.default_rng(seed)
+    lens = rng.integers(0, maxlen, n).astype(np.uint32)
+    edge = [0, 1, 7, 8, 9, 15, 16, 17, 31, 32, 33, 2040, 2041, 2048, 2049]
+    lens[: len(edge)] = edge[:n]
+    gaps = rng.integers(0, gap_max + 1, n)
+    in_off = np.zeros(n, np.uint64)
+    in_off[0] = base_misalign
+    in_off[1:] = base_misalign + np.cumsum((lens + gaps)[:-1], dtype=np.uint64)
+    inp = rng.integers(0, 256, int(in_off[-1] + lens[-1] + 64), dtype=np.uint8)
+    return lens, in_off, inp
+
+
+@pytest.mark.parametrize("obf", [True, False])
+@pytest.mark.parametrize("layout", ["packed", "slotted", "capped", "tiny"])
+def test_ragged_layouts_vs_oracle(obfs, gpu, coracle, obf, layout):
+    import torch
+    n = 3000 if layout != "tiny" else 1500
+    maxlen = 2100 if layout != "tiny" else 40
+    lens, in_off, inp = _ragged_case(21 + (layout == "tiny"), n, maxlen, 5, 3)
+    salts = ref.splitmix64_array(2, 0, n)
+    out_stride, pkt_cap = 0, 0
+    out_cap = int(lens.sum()) + 8 * n + 16
+    if layout == "slotted":
+        out_stride, out_cap = 2048, 2048 * n
+    elif layout == "capped":
+        pkt_cap, out_cap = 2048, out_cap // 2
+    exp, eoff, elen, etot = coracle.batch(obf, PSK, n, inp, in_off=in_off, in_len=lens,
+                                          salts=salts if obf else None, out_cap=out_cap,
+                                          out_stride=out_stride, pkt_cap=pkt_cap)
+    sentinel = 0xA5
+    out = torch.full((out_cap + 32,), sentinel, dtype=torch.uint8, device=gpu)
+    out_off = torch.empty(n, dtype=torch.int64, device=gpu)
+    out_len = torch.empty(n, dtype=torch.int32, device=gpu)
+    total = torch.zeros(1, dtype=torch.int64, device=gpu)
+    kw = dict(in_off=_u64(in_off, gpu), in_len=_u32(lens, gpu), out=out, out_cap=out_cap,
+              out_stride=out_stride, pkt_cap=pkt_cap, out_off=out_off, out_len=out_len, out_total=total)
+    if obf:
+        obfs.obfuscate_batch(_dev(inp, gpu), n, salts=_u64(salts, gpu), **kw)
+    else:
+        obfs.deobfuscate_batch(_dev(inp, gpu), n, **kw)
+    got = _host(out)
+    assert np.array_equal(_host(out_off).view(np.uint64), eoff)
+    assert np.array_equal(_host(out_len).view(np.uint32), elen)
+    assert int(_host(total)[0]) == etot
+    # written regions equal the oracle; everything else keeps the sentinel
+    written = np.zeros(out_cap + 32, bool)
+    for o, w in zip(eoff, elen):
+        written[int(o): int(o) + int(w)] = True
+    assert np.array_equal(got[:out_cap][written[:out_cap]], exp[written[:out_cap]])
+    assert (got[~written] == sentinel).all()
+
+
+def test_empty_batch(obfs, gpu):
+    import torch
+    out = torch.zeros(16, dtype=torch.uint8, device=gpu)
+    total = torch.full((1,), 7, dtype=torch.int64, device=gpu)
+    salts = torch.zeros(1, dtype=torch.int64, device=gpu)
+    obfs.obfuscate_batch(out, 0, salts=salts, out=out, out_total=total)
+    assert int(_host(total)[0]) == 0
+
+
+def test_misaligned_out_rejected(obfs, gpu):
+    import torch
+    from hysteria_amd._lib import HyobfsError
+    buf = torch.zeros(4096, dtype=torch.uint8, device=gpu)
+    salts = torch.zeros(1, dtype=torch.int64, device=gpu)
+    with pytest.raises(HyobfsError):
+        obfs.obfuscate_batch(buf, 1, len_uniform=10, salts=salts, out=buf.data_ptr() + 1, out_cap=100)
