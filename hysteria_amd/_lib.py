@@ -10,7 +10,7 @@ import os
 import re
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libhyobfs.so")
+LIB_PATH = os.environ.get("HYOBFS_LIB") or os.path.join(_HERE, "libhyobfs.so")
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "hyobfs.h")
 
 HYOBFS_OK = 0

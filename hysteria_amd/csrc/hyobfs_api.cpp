@@ -5,9 +5,14 @@
 // (RandSrc), and a lock for the per-packet path (lk).  It is bound to one
 // HIP device.  Every compute call runs the gfx950 kernels of salamander.hip;
 // there is no CPU path.
+#ifdef HYOBFS_EMULATE
+#include "hip_emu.h"   // tests/emu: CPU emulation for the CPU test tier, never shipped
+#else
 #include <hip/hip_runtime.h>
+#endif
 
 #include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
@@ -259,11 +264,30 @@ int run_batch(hyobfs_salamander* c, const hyobfs_batch* b, void* stream, bool ob
     if (!c || !b) return HYOBFS_ERR_INVALID;
     DeviceGuard g(c->device);
     if (!g.ok) return HYOBFS_ERR_HIP;
-    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : c->stream;
+    hipStream_t s = static_cast<hipStream_t>(stream);   // NULL = the HIP null stream
     BatchParams bp;
     const int rc = validate_and_fill(c, b, obf, bp, s);
     if (rc != HYOBFS_OK) return rc;
+#ifdef HY_BOUNDS_CHECK
+    // debug variant: HYOBFS_DEBUG_IN_BYTES bounds the input; report the first bad access
+    static unsigned long long* dbg = nullptr;
+    if (!dbg && hipMalloc(reinterpret_cast<void**>(&dbg), 16 * sizeof(unsigned long long)) != hipSuccess)
+        return HYOBFS_ERR_NOMEM;
+    (void)hipMemsetAsync(dbg, 0, 16 * sizeof(unsigned long long), s);
+    bp.dbg = dbg;
+    const char* ib = std::getenv("HYOBFS_DEBUG_IN_BYTES");
+    bp.dbg_in_bytes = ib ? std::strtoull(ib, nullptr, 10) : ~0ull;
+    const int r2 = hyobfs::launch_salamander(obf, bp, c->kp, s) == hipSuccess ? HYOBFS_OK : HYOBFS_ERR_HIP;
+    unsigned long long h[16];
+    (void)hipStreamSynchronize(s);
+    (void)hipMemcpy(h, dbg, sizeof h, hipMemcpyDeviceToHost);
+    if (h[0])
+        std::fprintf(stderr, "HY_BOUNDS kind=%llu block=%llu thread=%llu v=%llu %llu %llu %llx n=%llu\n", h[0], h[1],
+                     h[2], h[3], h[4], h[5], h[6], (unsigned long long)bp.n);
+    return r2;
+#else
     return hyobfs::launch_salamander(obf, bp, c->kp, s) == hipSuccess ? HYOBFS_OK : HYOBFS_ERR_HIP;
+#endif
 }
 
 }  // namespace
@@ -364,7 +388,7 @@ int hyobfs_salamander_keys_batch(hyobfs_salamander* c, const uint64_t* salts, ui
     if (!c || (n && (!salts || !keys))) return HYOBFS_ERR_INVALID;
     DeviceGuard g(c->device);
     if (!g.ok) return HYOBFS_ERR_HIP;
-    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : c->stream;
+    hipStream_t s = static_cast<hipStream_t>(stream);   // NULL = the HIP null stream
     return hyobfs::launch_keys(c->kp, salts, keys, n, s) == hipSuccess ? HYOBFS_OK : HYOBFS_ERR_HIP;
 }
 

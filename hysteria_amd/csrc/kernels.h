@@ -1,7 +1,11 @@
 // Private interface between the C ABI layer (hyobfs_api.cpp) and the gfx950
 // kernels (salamander.hip).  Not installed; include/hyobfs.h is the ABI.
 #pragma once
+#ifdef HYOBFS_EMULATE
+#include "hip_emu.h"   // tests/emu: CPU emulation for the CPU test tier, never shipped
+#else
 #include <hip/hip_runtime.h>
+#endif
 #include <stdint.h>
 
 namespace hyobfs {
@@ -41,6 +45,12 @@ struct BatchParams {
     unsigned long long* out_total;
     const uint64_t* tile_prefix;  // packed: exclusive prefix of tile sums (ntiles+1)
     uint64_t* tile_sums;          // packed: scratch, ntiles+1 entries
+    uint64_t part_len;            // main kernel: n / grid datagrams per workgroup ...
+    uint64_t part_rem;            // ... plus one for the first n % grid workgroups
+    // HY_BOUNDS_CHECK builds only (build_variants/, never the shipped library):
+    // first out-of-range access recorded here instead of performed
+    unsigned long long* dbg;
+    uint64_t dbg_in_bytes;
 };
 
 hipError_t launch_salamander(bool obfuscate, const BatchParams& b, const KeyParams& k,

@@ -1,0 +1,14 @@
+// salamander_inst.hip -- instantiates the main kernel for one salt word
+// (compiled once per HY_SW = 0..15, see Makefile).
+#include "salamander_device.h"
+
+#ifndef HY_SW
+#error "compile with -DHY_SW=<salt word 0..15>"
+#endif
+
+namespace hyobfs {
+template void launch_main_sw<true, true, HY_SW>(const BatchParams&, const KeyParams&, hipStream_t);
+template void launch_main_sw<true, false, HY_SW>(const BatchParams&, const KeyParams&, hipStream_t);
+template void launch_main_sw<false, true, HY_SW>(const BatchParams&, const KeyParams&, hipStream_t);
+template void launch_main_sw<false, false, HY_SW>(const BatchParams&, const KeyParams&, hipStream_t);
+}  // namespace hyobfs

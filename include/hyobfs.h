@@ -100,7 +100,7 @@ void hyobfs_salamander_next_salts(hyobfs_salamander* ctx, uint8_t* salts, size_t
 int hyobfs_salamander_key(hyobfs_salamander* ctx, const uint8_t salt[8],
                           uint8_t key[32]);
 /* keyLocked for n salts at once: keys[32*i..] = BLAKE2b-256(PSK || salts[i]).
-   Device pointers, enqueued on stream (NULL = the context's stream). */
+   Device pointers, enqueued on stream (a hipStream_t; NULL = the null stream). */
 int hyobfs_salamander_keys_batch(hyobfs_salamander* ctx, const uint64_t* salts,
                                  uint8_t* keys, uint64_t n, void* stream);
 /* Obfuscate (salamander.go:59-72) with an explicit salt.  Host buffers, synchronous. */
@@ -139,8 +139,8 @@ size_t hyobfs_salamander_deobfuscate(hyobfs_salamander* ctx, const uint8_t* in,
  *             Bytes of `out` outside valid regions are not written.
  *
  * `out` must be 16-byte aligned.  All pointers are device-accessible; the
- * call only enqueues work on `stream` (a hipStream_t; NULL = the context's
- * own stream) and returns.  workspace: device scratch of at least
+ * call only enqueues work on `stream` (a hipStream_t; NULL = the HIP null
+ * stream, as everywhere in HIP) and returns.  workspace: device scratch of at least
  * hyobfs_batch_workspace_size(n) bytes, or NULL to use a context-owned buffer
  * (then the first call of a new maximum size allocates and is not
  * graph-capturable).

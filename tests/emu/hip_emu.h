@@ -1,0 +1,188 @@
+// hip_emu.h -- CPU emulation of the HIP subset used by hysteria_amd/csrc.
+//
+// TEST INFRASTRUCTURE ONLY.  tests/emu/build.sh compiles the unmodified kernel
+// and ABI sources with clang for x86-64 against this header (-DHYOBFS_EMULATE),
+// into tests/emu/libhyobfs_emu.so, under AddressSanitizer.  That library is
+// never shipped or loaded by the product package: it lets the CPU test tier
+// run the kernels' logic (indexing, ownership, scans, pipelining) against the
+// oracle and catch out-of-bounds accesses before a kernel ever reaches a GPU.
+//
+// Model: a launch runs its workgroups one after another; a workgroup runs as
+// blockDim.x std::threads.  __syncthreads is a barrier of the workgroup,
+// wavefront operations (__shfl_*, readfirstlane) exchange values through a
+// per-wave slot array between two barriers of the 64 lanes.  __shared__
+// variables are function-local statics (one workgroup at a time).  All lanes
+// are assumed active at every wavefront operation, which the kernels satisfy
+// (they only shuffle in wave-uniform code).
+#pragma once
+#include <algorithm>
+#include <atomic>
+#include <barrier>
+#include <cstdint>
+#include <cstdlib>
+#include <cstring>
+#include <memory>
+#include <thread>
+#include <vector>
+
+#define __global__
+#define __device__
+#define __host__
+#define __forceinline__ inline
+#define __launch_bounds__(...)
+#define __shared__ static
+
+struct dim3 {
+    uint32_t x = 1, y = 1, z = 1;
+    dim3(uint32_t a = 1, uint32_t b = 1, uint32_t c = 1) : x(a), y(b), z(c) {}
+};
+struct uint4 {
+    uint32_t x, y, z, w;
+};
+inline uint4 make_uint4(uint32_t a, uint32_t b, uint32_t c, uint32_t d) { return uint4{a, b, c, d}; }
+
+typedef int hipError_t;
+typedef void* hipStream_t;
+typedef void* hipEvent_t;
+enum { hipSuccess = 0, hipErrorInvalidValue = 1, hipErrorOutOfMemory = 2 };
+enum { hipHostMallocMapped = 2, hipStreamNonBlocking = 1 };
+enum hipDeviceAttribute_t { hipDeviceAttributeMultiprocessorCount = 0 };
+struct hipDeviceProp_t {
+    char gcnArchName[256];
+};
+
+namespace hyemu {
+struct Ctx {
+    std::barrier<>* block = nullptr;
+    std::barrier<>* wave[16] = {};
+    uint64_t slots[1024];
+};
+inline Ctx g_ctx;
+inline thread_local dim3 t_thread, t_block;
+inline dim3 g_grid, g_blockdim;
+inline int env_int(const char* k, int d) {
+    const char* v = std::getenv(k);
+    return v ? std::atoi(v) : d;
+}
+inline int g_cus = env_int("HYEMU_CUS", 4), g_per_cu = env_int("HYEMU_PER_CU", 1);
+
+template <class T>
+inline T xchg(T v, int src_lane) {
+    const int t = (int)t_thread.x, lane = t & 63, w = t >> 6;
+    uint64_t bits = 0;
+    static_assert(sizeof(T) <= 8, "shuffle of a value wider than 64 bits");
+    std::memcpy(&bits, &v, sizeof(T));
+    g_ctx.slots[t] = bits;
+    g_ctx.wave[w]->arrive_and_wait();
+    T out = v;
+    if (src_lane >= 0 && src_lane < 64) std::memcpy(&out, &g_ctx.slots[w * 64 + src_lane], sizeof(T));
+    g_ctx.wave[w]->arrive_and_wait();
+    return out;
+}
+
+template <class F>
+inline void launch(dim3 grid, dim3 block, F&& body) {
+    g_grid = grid;
+    g_blockdim = block;
+    const uint32_t nt = block.x;
+    for (uint32_t b = 0; b < grid.x; ++b) {
+        std::barrier<> bar((std::ptrdiff_t)nt);
+        std::vector<std::unique_ptr<std::barrier<>>> waves;
+        for (uint32_t w = 0; w < (nt + 63) / 64; ++w) {
+            waves.emplace_back(new std::barrier<>((std::ptrdiff_t)std::min<uint32_t>(64, nt - 64 * w)));
+            g_ctx.wave[w] = waves.back().get();
+        }
+        g_ctx.block = &bar;
+        std::vector<std::thread> th;
+        th.reserve(nt);
+        for (uint32_t t = 0; t < nt; ++t)
+            th.emplace_back([&, t, b] {
+                t_thread = dim3(t);
+                t_block = dim3(b);
+                body();
+            });
+        for (auto& x : th) x.join();
+    }
+}
+}  // namespace hyemu
+
+#define threadIdx (hyemu::t_thread)
+#define blockIdx (hyemu::t_block)
+#define gridDim (hyemu::g_grid)
+#define blockDim (hyemu::g_blockdim)
+
+inline void __syncthreads() { hyemu::g_ctx.block->arrive_and_wait(); }
+
+template <class T>
+inline T __shfl_up(T v, unsigned d, int width = 64) {
+    (void)width;
+    const int lane = (int)(threadIdx.x & 63);
+    T r = hyemu::xchg(v, lane - (int)d);
+    return lane >= (int)d ? r : v;
+}
+template <class T>
+inline T __shfl_xor(T v, int m, int width = 64) {
+    (void)width;
+    return hyemu::xchg(v, (int)(threadIdx.x & 63) ^ m);
+}
+template <class T>
+inline T __shfl(T v, int src, int width = 64) {
+    (void)width;
+    return hyemu::xchg(v, src);
+}
+// like the builtin: int in, int out (a caller that widens the result must
+// convert it to unsigned first, exactly as on the GPU)
+inline int hyemu_readfirstlane(int v) { return hyemu::xchg(v, 0); }
+#define __builtin_amdgcn_readfirstlane(x) hyemu_readfirstlane((int)(x))
+inline uint32_t hyemu_alignbit(uint32_t hi, uint32_t lo, uint32_t s) {
+    return (uint32_t)((((uint64_t)hi << 32) | lo) >> (s & 31));
+}
+#define __builtin_amdgcn_alignbit(a, b, c) hyemu_alignbit((a), (b), (c))
+
+template <class T>
+inline T min(T a, T b) { return a < b ? a : b; }
+template <class T>
+inline T max(T a, T b) { return a < b ? b : a; }
+
+inline unsigned long long atomicCAS(unsigned long long* p, unsigned long long cmp, unsigned long long v) {
+    __atomic_compare_exchange_n(p, &cmp, v, false, __ATOMIC_RELAXED, __ATOMIC_RELAXED);
+    return cmp;
+}
+enum { hipMemcpyDeviceToHost = 2 };
+inline int hipMemcpy(void* d, const void* s, size_t n, int) { std::memcpy(d, s, n); return 0; }
+inline unsigned long long atomicAdd(unsigned long long* p, unsigned long long v) {
+    return __atomic_fetch_add(p, v, __ATOMIC_RELAXED);
+}
+
+#define hipLaunchKernelGGL(kernel, grid, block, shmem, stream, ...) \
+    hyemu::launch(dim3(grid), dim3(block), [&] { kernel(__VA_ARGS__); })
+
+// ---- runtime API subset
+inline hipError_t hipGetLastError() { return hipSuccess; }
+inline const char* hipGetErrorString(hipError_t) { return "emulated"; }
+inline hipError_t hipGetDeviceCount(int* n) { *n = 1; return hipSuccess; }
+inline hipError_t hipGetDevice(int* d) { *d = 0; return hipSuccess; }
+inline hipError_t hipSetDevice(int d) { return d == 0 ? hipSuccess : hipErrorInvalidValue; }
+inline hipError_t hipGetDeviceProperties(hipDeviceProp_t* p, int) {
+    std::strcpy(p->gcnArchName, "gfx950:emulated");
+    return hipSuccess;
+}
+inline hipError_t hipDeviceGetAttribute(int* v, hipDeviceAttribute_t, int) { *v = hyemu::g_cus; return hipSuccess; }
+template <class K>
+inline hipError_t hipOccupancyMaxActiveBlocksPerMultiprocessor(int* nb, K, int, size_t) {
+    *nb = hyemu::g_per_cu;
+    return hipSuccess;
+}
+inline hipError_t hipStreamCreateWithFlags(hipStream_t* s, unsigned) { *s = (hipStream_t)1; return hipSuccess; }
+inline hipError_t hipStreamDestroy(hipStream_t) { return hipSuccess; }
+inline hipError_t hipStreamSynchronize(hipStream_t) { return hipSuccess; }
+inline hipError_t hipDeviceSynchronize() { return hipSuccess; }
+inline hipError_t hipMalloc(void** p, size_t n) {
+    *p = std::malloc(n ? n : 1);
+    return *p ? hipSuccess : hipErrorOutOfMemory;
+}
+inline hipError_t hipFree(void* p) { std::free(p); return hipSuccess; }
+inline hipError_t hipHostMalloc(void** p, size_t n, unsigned) { return hipMalloc(p, n); }
+inline hipError_t hipHostFree(void* p) { return hipFree(p); }
+inline hipError_t hipHostGetDevicePointer(void** d, void* h, unsigned) { *d = h; return hipSuccess; }
+inline hipError_t hipMemsetAsync(void* p, int v, size_t n, hipStream_t) { std::memset(p, v, n); return hipSuccess; }

@@ -1,0 +1,135 @@
+"""Run batches through the CPU-emulated kernels (tests/emu/libhyobfs_emu.so)
+and compare with the C oracle.  Invoked by tests/test_emulated_kernels.py in a
+subprocess with the ASan runtime preloaded."""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, ROOT)
+import numpy as np  # noqa: E402
+
+os.environ.setdefault("HYOBFS_LIB", os.path.join(ROOT, "tests", "emu", "libhyobfs_emu.so"))
+from hysteria_amd import _lib  # noqa: E402
+from hysteria_amd.salamander import SalamanderObfuscator  # noqa: E402
+from oracle import salamander_ref as ref  # noqa: E402
+
+
+def run(obf, psk, lens, in_off, inp, salts, out_cap, out_stride=0, pkt_cap=0, in_stride=0, len_uniform=0):
+    n = len(lens) if lens is not None else len(salts)
+    co = ref.COracle()
+    exp, eoff, elen, etot = co.batch(obf, psk, n, inp, in_off=in_off, in_stride=in_stride, in_len=lens,
+                                     len_uniform=len_uniform, salts=salts if obf else None, out_cap=out_cap,
+                                     out_stride=out_stride, pkt_cap=pkt_cap)
+    out = np.full(out_cap + 64, 0xA5, np.uint8)
+    out_off = np.zeros(max(n, 1), np.uint64)
+    out_len = np.zeros(max(n, 1), np.uint32)
+    total = np.zeros(1, np.uint64)
+    o = SalamanderObfuscator(psk, 0)
+    p = lambda a: None if a is None else a.ctypes.data  # noqa: E731
+    kw = dict(in_off=p(in_off), in_stride=in_stride, in_len=p(lens), len_uniform=len_uniform, out=p(out),
+              out_cap=out_cap, out_stride=out_stride, pkt_cap=pkt_cap, out_off=p(out_off), out_len=p(out_len),
+              out_total=p(total), stream=0)
+    if obf:
+        o.obfuscate_batch(p(inp), n, salts=p(salts), **kw)
+    else:
+        o.deobfuscate_batch(p(inp), n, **kw)
+    o.close()
+    assert np.array_equal(out_off[:n], eoff), "out_off"
+    assert np.array_equal(out_len[:n], elen), "out_len"
+    assert int(total[0]) == etot, ("total", int(total[0]), etot)
+    written = np.zeros(out_cap + 64, bool)
+    for off, w in zip(eoff, elen):
+        written[int(off):int(off) + int(w)] = True
+    bad = np.nonzero(written[:out_cap] & (out[:out_cap] != exp))[0]
+    assert bad.size == 0, ("mismatch", bad[:10], bad.size)
+    assert (out[~written] == 0xA5).all(), "wrote outside regions"
+
+
+def case_ragged(seed, n, maxlen, obf, layout, psk=b"average_password"):
+    rng = np.random.default_rng(seed)
+    lens = rng.integers(0, maxlen, n).astype(np.uint32)
+    gaps = rng.integers(0, 4, n)
+    in_off = np.zeros(n, np.uint64)
+    in_off[0] = 5
+    in_off[1:] = 5 + np.cumsum((lens + gaps)[:-1], dtype=np.uint64)
+    inp = rng.integers(0, 256, int(in_off[-1] + lens[-1] + 32), dtype=np.uint8)
+    salts = ref.splitmix64_array(2, 0, n)
+    cap = int(lens.sum()) + 8 * n + 16
+    stride = 0
+    if layout == "slotted":
+        stride = maxlen + 8
+        cap = stride * n
+    run(obf, psk, lens, in_off, inp, salts, cap, out_stride=stride)
+
+
+def case_bimodal(n, obf):
+    lens = ref.bimodal_lengths(3, 0, n)
+    in_off = np.zeros(n, np.uint64)
+    in_off[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+    inp = np.frombuffer(ref.stream_bytes(1, 0, int(lens.sum()) + 16), np.uint8).copy()
+    salts = ref.splitmix64_array(2, 0, n)
+    if not obf:   # feed real wire bytes
+        co = ref.COracle()
+        cap = int(lens.sum()) + 8 * n
+        wire, woff, wlen, _ = co.batch(True, b"average_password", n, inp, in_off=in_off, in_len=lens, salts=salts,
+                                       out_cap=cap)
+        run(False, b"average_password", wlen, woff, wire, None, int(lens.sum()) + 16)
+    else:
+        run(True, b"average_password", lens, in_off, inp, salts, int(lens.sum()) + 8 * n)
+
+
+def case_uniform(n, L, obf):
+    inp = np.frombuffer(ref.stream_bytes(1, 0, n * (L + 8) + 16), np.uint8).copy()
+    salts = ref.splitmix64_array(2, 0, n)
+    if obf:
+        run(True, b"average_password", None, None, inp, salts, n * (L + 8), out_stride=L + 8, in_stride=L,
+            len_uniform=L)
+    else:
+        run(False, b"average_password", None, None, inp, salts, n * L, out_stride=L, in_stride=L + 8,
+            len_uniform=L + 8)
+
+
+def case_slotted_far(n, L, stride_mb, obf):
+    """Slotted output whose slots sit beyond 2^31: the output buffer is an untouched
+    anonymous mapping, so only the written slots cost memory."""
+    import mmap
+    stride = stride_mb << 20
+    cap = n * stride
+    mm = mmap.mmap(-1, cap + 4096)
+    out = np.frombuffer(mm, np.uint8)
+    rng = np.random.default_rng(n)
+    inp = rng.integers(0, 256, n * L + 64, dtype=np.uint8)
+    salts = ref.splitmix64_array(2, 0, n)
+    o = SalamanderObfuscator(b"average_password", 0)
+    if obf:
+        o.obfuscate_batch(inp.ctypes.data, n, in_stride=L, len_uniform=L, salts=salts.ctypes.data,
+                          out=out.ctypes.data, out_cap=cap, out_stride=stride, stream=0)
+    else:
+        o.deobfuscate_batch(inp.ctypes.data, n, in_stride=L, len_uniform=L, out=out.ctypes.data, out_cap=cap,
+                            out_stride=stride, stream=0)
+    o.close()
+    for i in range(n):
+        src = inp[i * L:(i + 1) * L].tobytes()
+        exp = ref.obfuscate(b"average_password", src, int(salts[i]).to_bytes(8, "little")) if obf \
+            else ref.deobfuscate(b"average_password", src)
+        got = out[i * stride:i * stride + len(exp)].tobytes()
+        assert got == exp, i
+        assert not out[i * stride + len(exp):i * stride + len(exp) + 16].any()
+    del out
+    mm.close()
+
+
+if __name__ == "__main__":
+    lib = _lib.load()
+    which = sys.argv[1]
+    args = [int(a) for a in sys.argv[2:]]
+    if which == "bimodal":
+        case_bimodal(args[0], bool(args[1]))
+    elif which == "uniform":
+        case_uniform(args[0], args[1], bool(args[2]))
+    elif which == "far":
+        case_slotted_far(args[0], args[1], args[2], bool(args[3]))
+    elif which == "ragged":
+        case_ragged(args[0], args[1], args[2], bool(args[3]), ["packed", "slotted"][args[4]])
+    print("ok", which, args)
+

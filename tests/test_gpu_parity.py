@@ -308,3 +308,72 @@ def test_misaligned_out_rejected(obfs, gpu):
     salts = torch.zeros(1, dtype=torch.int64, device=gpu)
     with pytest.raises(HyobfsError):
         obfs.obfuscate_batch(buf, 1, len_uniform=10, salts=salts, out=buf.data_ptr() + 1, out_cap=100)
+
+
+# PSK lengths that put salt[0] in every message word 0..15 (aligned and not),
+# the two-block tail (121..127 mod 128) and multi-block PSKs
+PSK_SWEEP = [4, 5, 8, 13, 16, 23, 24, 31, 36, 40, 47, 52, 56, 63, 64, 71, 72, 79, 80, 88, 95,
+             96, 100, 104, 111, 112, 119, 120, 121, 124, 127, 128, 129, 200, 248, 249, 255, 256, 300]
+
+
+@pytest.mark.parametrize("psk_len", PSK_SWEEP)
+@pytest.mark.parametrize("obf", [True, False])
+def test_every_salt_word_instantiation(gpu, coracle, psk_len, obf):
+    import torch
+    import hysteria_amd
+    psk = ref.stream_bytes(11, 0, psk_len)
+    n = 700
+    lens, in_off, inp = _ragged_case(100 + psk_len, n, 1500, 3, 1)
+    salts = ref.splitmix64_array(5, 0, n)
+    out_cap = int(lens.sum()) + 8 * n + 16
+    exp, eoff, elen, _ = coracle.batch(obf, psk, n, inp, in_off=in_off, in_len=lens,
+                                       salts=salts if obf else None, out_cap=out_cap)
+    out = torch.zeros(out_cap, dtype=torch.uint8, device=gpu)
+    out_len = torch.empty(n, dtype=torch.int32, device=gpu)
+    with hysteria_amd.SalamanderObfuscator(psk, 0) as o:
+        kw = dict(in_off=_u64(in_off, gpu), in_len=_u32(lens, gpu), out=out, out_cap=out_cap, out_len=out_len)
+        if obf:
+            o.obfuscate_batch(_dev(inp, gpu), n, salts=_u64(salts, gpu), **kw)
+        else:
+            o.deobfuscate_batch(_dev(inp, gpu), n, **kw)
+        got = _host(out)
+    assert np.array_equal(_host(out_len).view(np.uint32), elen)
+    assert np.array_equal(got, exp)
+
+
+def test_packed_output_offsets_beyond_4GiB(obfs, gpu):
+    """Packed output of 4.6 GB: offsets past 2^31 and 2^32 (64-bit offset arithmetic).
+    Inputs alias one 1 MiB region (in_off is free-form), so only the output is large."""
+    import torch
+    n, L = 3_400_000, 1350
+    region = 1 << 20
+    src = torch.empty(region, dtype=torch.uint8, device=gpu)
+    import hysteria_amd
+    hysteria_amd.synth_stream(src, region, 1, 0)
+    idx = torch.arange(n, dtype=torch.int64, device=gpu)
+    in_off = (idx * 977) % (region - L)
+    lens = torch.full((n,), L, dtype=torch.int32, device=gpu)
+    salts = torch.empty(n, dtype=torch.int64, device=gpu)
+    hysteria_amd.synth_u64(salts, n, 2, 0)
+    cap = n * (L + 8)
+    assert cap > (1 << 32)
+    out = torch.empty(cap, dtype=torch.uint8, device=gpu)
+    out_off = torch.empty(n, dtype=torch.int64, device=gpu)
+    out_len = torch.empty(n, dtype=torch.int32, device=gpu)
+    obfs.obfuscate_batch(src, n, in_off=in_off, in_len=lens, salts=salts, out=out, out_cap=cap,
+                         out_off=out_off, out_len=out_len)
+    torch.cuda.synchronize()
+    assert torch.equal(out_off, idx * (L + 8))
+    assert bool((out_len == L + 8).all())
+    h_src = src.cpu().numpy().tobytes()
+    h_salts = salts.cpu().numpy().view(np.uint64)
+    picks = set(range(0, n, 9973)) | {n - 1}
+    for edge in ((1 << 31), (1 << 32)):
+        p = edge // (L + 8)
+        picks |= {p - 1, p, p + 1}
+    for p in sorted(picks):
+        o = int(p) * (L + 8)
+        got = out[o:o + L + 8].cpu().numpy().tobytes()
+        io = (int(p) * 977) % (region - L)
+        exp = ref.obfuscate(PSK, h_src[io:io + L], int(h_salts[p]).to_bytes(8, "little"))
+        assert got == exp, p
