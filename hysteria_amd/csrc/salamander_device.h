@@ -625,44 +625,44 @@ __global__ __launch_bounds__(kTile) void salamander_kernel(BatchParams B, KeyPar
 
         const uint32_t steps = has_next ? nsteps : 0u;
         if (has_next) prep_load(s + 1);
-        SweepRegs R;
-        if (n_iters) issue(0, R);
-        const uint32_t n_loop = max(n_iters, steps);
-        for (uint32_t it = 0; it < n_loop; ++it) {
-            if (it < n_iters) {   // iteration it+1's loads fly while it is stored
-                SweepRegs Rn;
-                if (it + 1 < n_iters) issue(it + 1, Rn);
-                retire(it, R);
-                R = Rn;
+        auto boundary = [&]() {   // chunks datagram t owns that are not inside one payload
+            if ((uint32_t)t < cnt && T.w[t]) {
+                const uint32_t st = T.o[t], en = st + T.w[t];
+                const uint32_t cs = st >> 4, ce = (en - 1) >> 4;
+                const bool own_cs = T.pe[t] <= (cs << 4);
+                const uint32_t cand[3] = {cs, cs + 1, ce};
+                const bool use[3] = {own_cs, cs + 1 <= ce, ce > cs + 1};
+#pragma unroll
+                for (int i = 0; i < 3; ++i) {
+                    if (!use[i]) continue;
+                    const uint32_t a = cand[i] << 4;
+                    if (st + SALT <= a && a + 16 <= en) continue;   // inside the payload: swept
+                    u128 r = 0;
+                    uint32_t cov = 0;
+                    for (uint32_t k = t; k < cnt && T.o[k] < a + 16; ++k) chunk_contrib<OBF>(B, T, in, k, a, r, cov);
+                    if (cov && HY_OK(3, (uint64_t)(outb - B.out) + a + 16 <= B.out_cap + 15, (uint64_t)(outb - B.out),
+                                     a, cov, s))
+                        store_masked(outb + a, r, cov);
+                }
             }
+        };
+        // Sweep iteration it: issue its loads; while they fly, finish the
+        // boundary chunks (iteration 0) and run one round of the next
+        // sub-tile's hash; then XOR and store.  (A one-iteration-ahead prefetch
+        // measured slower: its registers cost a wave per SIMD.)
+        const uint32_t n_loop = max(max(n_iters, steps + 1), cnt ? 1u : 0u);
+        for (uint32_t it = 0; it < n_loop; ++it) {
+            SweepRegs R;
+            if (it < n_iters) issue(it, R);
+            if (it == 0) boundary();
+            if (it >= 1 && it <= steps) hash_step<SW>(hs, K, it - 1);
+            if (it < n_iters) retire(it, R);
             if (it == 0 && has_next) {
                 prep_finish(s + 1, N);
                 hash_begin<SW>(hs, K, psalt);
             }
-            if (it < steps) hash_step<SW>(hs, K, it);
         }
         if (has_next) finish_key(N);
-
-        // boundary chunks owned by datagram t
-        if ((uint32_t)t < cnt && T.w[t]) {
-            const uint32_t st = T.o[t], en = st + T.w[t];
-            const uint32_t cs = st >> 4, ce = (en - 1) >> 4;
-            const bool own_cs = T.pe[t] <= (cs << 4);
-            const uint32_t cand[3] = {cs, cs + 1, ce};
-            const bool use[3] = {own_cs, cs + 1 <= ce, ce > cs + 1};
-#pragma unroll
-            for (int i = 0; i < 3; ++i) {
-                if (!use[i]) continue;
-                const uint32_t a = cand[i] << 4;
-                if (st + SALT <= a && a + 16 <= en) continue;   // inside the payload: swept
-                u128 r = 0;
-                uint32_t cov = 0;
-                for (uint32_t k = t; k < cnt && T.o[k] < a + 16; ++k) chunk_contrib<OBF>(B, T, in, k, a, r, cov);
-                if (cov && HY_OK(3, (uint64_t)(outb - B.out) + a + 16 <= B.out_cap + 15, (uint64_t)(outb - B.out),
-                                 a, cov, s))
-                    store_masked(outb + a, r, cov);
-            }
-        }
         __syncthreads();
     }
 

@@ -1,0 +1,31 @@
+"""Minimal driver for rocprofv3 counter passes: K obfuscate + K deobfuscate launches
+of the uniform 1M x 1200 B batch (BASELINE configs[1]), or bimodal with 'bimodal'."""
+import os, sys
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch, hysteria_amd
+wl = sys.argv[1] if len(sys.argv) > 1 else "uniform"
+K = int(sys.argv[2]) if len(sys.argv) > 2 else 5
+dev = torch.device("cuda:0")
+o = hysteria_amd.SalamanderObfuscator(b"average_password", 0)
+if wl == "uniform":
+    P, L = 1 << 20, 1200
+    inp = torch.empty(P * L, dtype=torch.uint8, device=dev); hysteria_amd.synth_stream(inp, P * L, 1, 0)
+    salts = torch.empty(P, dtype=torch.int64, device=dev); hysteria_amd.synth_u64(salts, P, 2, 0)
+    wire = torch.empty(P * (L + 8), dtype=torch.uint8, device=dev); back = torch.empty(P * L, dtype=torch.uint8, device=dev)
+    for _ in range(K):
+        o.obfuscate_batch(inp, P, in_stride=L, len_uniform=L, salts=salts, out=wire, out_stride=L + 8)
+    for _ in range(K):
+        o.deobfuscate_batch(wire, P, in_stride=L + 8, len_uniform=L + 8, out=back, out_stride=L)
+else:
+    P = 1 << 22
+    lens = torch.empty(P, dtype=torch.int32, device=dev); hysteria_amd.synth_bimodal_lengths(lens, P, 3, 0)
+    in_off = torch.zeros(P, dtype=torch.int64, device=dev); in_off[1:] = torch.cumsum(lens[:-1].to(torch.int64), 0)
+    total_in = int(lens.to(torch.int64).sum())
+    inp = torch.empty(total_in + 16, dtype=torch.uint8, device=dev); hysteria_amd.synth_stream(inp, total_in, 1, 0)
+    salts = torch.empty(P, dtype=torch.int64, device=dev); hysteria_amd.synth_u64(salts, P, 2, 0)
+    cap = total_in + 8 * P
+    wire = torch.empty(cap, dtype=torch.uint8, device=dev)
+    for _ in range(K):
+        o.obfuscate_batch(inp, P, in_off=in_off, in_len=lens, salts=salts, out=wire, out_cap=cap)
+torch.cuda.synchronize()
+print("done", wl, K)
