@@ -104,12 +104,15 @@ def main():
     import torch
     import torch.distributed as dist
     import hysteria_amd
+    from hysteria_amd.shard import weak_shard
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         dist.init_process_group("gloo", init_method="env://")
+    # one process per GPU; modulo the visible devices so N > 1 can be rehearsed on one card
+    local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
@@ -130,7 +133,7 @@ def main():
 
     if args.workload == "uniform":
         P = args.packets_per_gpu or (1 << 20)
-        first = rank * P
+        first, P = weak_shard(P, rank)
         inp = torch.empty(P * L, dtype=torch.uint8, device=dev)
         hysteria_amd.synth_stream(inp, P * L, 1, first * L)
         salts = torch.empty(P, dtype=torch.int64, device=dev)
@@ -152,7 +155,7 @@ def main():
                   "psk": PSK.decode(), "parallelism": f"packet-index shards x{world}"}
     else:
         P = args.packets_per_gpu or (1 << 22)
-        first = rank * P
+        first, P = weak_shard(P, rank)
         lens = torch.empty(P, dtype=torch.int32, device=dev)
         hysteria_amd.synth_bimodal_lengths(lens, P, 3, first)
         in_off = torch.zeros(P, dtype=torch.int64, device=dev)

@@ -1,0 +1,50 @@
+"""Packet-index sharding across GPUs.
+
+Every datagram depends only on (PSK, salt, payload), so a batch shards by
+datagram index with no exchange step: rank r of W processes a contiguous
+range and writes its own output.  No collective is needed on the data path.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+
+def even_split(n: int, world: int, rank: int) -> tuple[int, int]:
+    """(first, count) of rank's contiguous share of n datagrams; counts differ by <= 1."""
+    if world < 1 or not 0 <= rank < world:
+        raise ValueError("bad world/rank")
+    q, r = divmod(n, world)
+    first = rank * q + min(rank, r)
+    return first, q + (1 if rank < r else 0)
+
+
+def byte_balanced_split(lengths: np.ndarray, world: int, rank: int) -> tuple[int, int]:
+    """(first, count) splitting a ragged batch so each rank gets ~equal payload bytes.
+
+    Boundary k sits at the first datagram whose exclusive byte prefix reaches
+    k/world of the total ("split by cumulative bytes").
+    """
+    if world < 1 or not 0 <= rank < world:
+        raise ValueError("bad world/rank")
+    lengths = np.asarray(lengths, dtype=np.uint64)
+    n = lengths.size
+    if n == 0:
+        return 0, 0
+    excl = np.zeros(n + 1, dtype=np.uint64)
+    np.cumsum(lengths, out=excl[1:])
+    total = int(excl[-1])
+
+    def cut(k: int) -> int:
+        if k <= 0:
+            return 0
+        if k >= world:
+            return n
+        return int(np.searchsorted(excl[:-1], total * k // world, side="left"))
+
+    a, b = cut(rank), cut(rank + 1)
+    return a, b - a
+
+
+def weak_shard(per_rank: int, rank: int) -> tuple[int, int]:
+    """Weak scaling: rank r owns datagrams [r*per_rank, (r+1)*per_rank) of the global batch."""
+    return rank * per_rank, per_rank
