@@ -89,6 +89,10 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         "hyobfs_batch_workspace_size": (u64, [u64]),
         "hyobfs_salamander_obfuscate_batch": (i32, [pctx, ctypes.POINTER(HyobfsBatch), vp]),
         "hyobfs_salamander_deobfuscate_batch": (i32, [pctx, ctypes.POINTER(HyobfsBatch), vp]),
+        "hyobfs_salamander_obfuscate_host": (i32, [pctx, ctypes.POINTER(HyobfsBatch), u64]),
+        "hyobfs_salamander_deobfuscate_host": (i32, [pctx, ctypes.POINTER(HyobfsBatch), u64]),
+        "hyobfs_host_alloc": (vp, [sz]),
+        "hyobfs_host_free": (None, [vp]),
         "hyobfs_synth_stream": (i32, [vp, u64, u64, u64, vp]),
         "hyobfs_synth_u64": (i32, [vp, u64, u64, u64, vp]),
         "hyobfs_synth_bimodal_lengths": (i32, [vp, u64, u64, u64, vp]),

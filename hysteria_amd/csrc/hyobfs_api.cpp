@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 #endif
 
+#include <algorithm>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -39,6 +40,18 @@ struct hyobfs_salamander {
     // context-owned batch workspace
     void* ws = nullptr;
     uint64_t ws_cap = 0;
+    // host-batch pipeline: three slots, one stream each (see *_host)
+    struct Slot {
+        hipStream_t s = nullptr;
+        uint8_t* in = nullptr;      // chunk x in_stride
+        uint8_t* out = nullptr;     // chunk x out_stride
+        uint32_t* len = nullptr;    // chunk
+        uint64_t* salts = nullptr;  // chunk
+        uint32_t* olen = nullptr;   // chunk
+        void* ws = nullptr;
+        uint64_t in_cap = 0, out_cap = 0, n_cap = 0, ws_cap = 0;
+    } slot[3];
+    std::mutex pipe_mu;
 };
 
 namespace {
@@ -290,6 +303,97 @@ int run_batch(hyobfs_salamander* c, const hyobfs_batch* b, void* stream, bool ob
 #endif
 }
 
+
+// Grow a device buffer (caller holds the pipeline lock; the slot's stream is idle).
+template <class T>
+int grow(T*& p, uint64_t& cap, uint64_t need_bytes) {
+    if (cap >= need_bytes && p) return HYOBFS_OK;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    void* q = nullptr;
+    if (hipMalloc(&q, need_bytes ? need_bytes : 16) != hipSuccess) return HYOBFS_ERR_NOMEM;
+    p = static_cast<T*>(q);
+    cap = need_bytes;
+    return HYOBFS_OK;
+}
+
+// Host batch through the three-slot pipeline: H2D(k) | kernels(k) | D2H(k) on
+// slot k % 3's stream; streams overlap each other, so the copy engines and
+// the compute queue work on different chunks at once.
+int run_host(hyobfs_salamander* c, const hyobfs_batch* b, uint64_t chunk, bool obf) {
+    if (!c || !b) return HYOBFS_ERR_INVALID;
+    if (b->n == 0) return HYOBFS_OK;
+    if (!b->in || !b->out || b->in_off || b->in_stride == 0 || b->out_stride == 0) return HYOBFS_ERR_INVALID;
+    if (obf && !b->salts) return HYOBFS_ERR_INVALID;
+    if (b->out_stride > hyobfs::kMaxDatagram) return HYOBFS_ERR_INVALID;
+    if (b->out_cap < b->n * b->out_stride) return HYOBFS_ERR_INVALID;
+    DeviceGuard g(c->device);
+    if (!g.ok) return HYOBFS_ERR_HIP;
+    std::lock_guard<std::mutex> lk(c->pipe_mu);
+    if (chunk == 0) chunk = std::max<uint64_t>(4096, (64ull << 20) / std::max<uint64_t>(b->in_stride, 1));
+    chunk = std::min<uint64_t>(chunk, b->n);
+    const uint64_t in_bytes = chunk * b->in_stride, out_bytes = chunk * b->out_stride;
+    for (auto& sl : c->slot) {
+        if (!sl.s && hipStreamCreateWithFlags(&sl.s, hipStreamNonBlocking) != hipSuccess) return HYOBFS_ERR_HIP;
+        uint64_t dummy = 0;
+        int rc = HYOBFS_OK;
+        if (sl.in_cap < in_bytes) rc |= grow(sl.in, sl.in_cap, in_bytes);
+        if (sl.out_cap < out_bytes) rc |= grow(sl.out, sl.out_cap, out_bytes);
+        if (sl.n_cap < chunk) {
+            uint64_t c1 = 0, c2 = 0, c3 = 0;
+            rc |= grow(sl.len, c1, chunk * 4);
+            rc |= grow(sl.salts, c2, chunk * 8);
+            rc |= grow(sl.olen, c3, chunk * 4);
+            sl.n_cap = chunk;
+        }
+        const uint64_t ws_need = hyobfs_batch_workspace_size(chunk);
+        if (sl.ws_cap < ws_need) rc |= grow(sl.ws, sl.ws_cap, ws_need);
+        (void)dummy;
+        if (rc != HYOBFS_OK) return HYOBFS_ERR_NOMEM;
+    }
+    const uint64_t nchunks = (b->n + chunk - 1) / chunk;
+    for (uint64_t k = 0; k < nchunks; ++k) {
+        auto& sl = c->slot[k % 3];
+        const uint64_t first = k * chunk, m = std::min<uint64_t>(chunk, b->n - first);
+        hipStream_t s = sl.s;
+        // slot reuse: the previous chunk on this stream is ordered before us
+        if (hipMemcpyAsync(sl.in, b->in + first * b->in_stride, m * b->in_stride, hipMemcpyHostToDevice, s) !=
+            hipSuccess)
+            return HYOBFS_ERR_HIP;
+        if (b->in_len &&
+            hipMemcpyAsync(sl.len, b->in_len + first, m * 4, hipMemcpyHostToDevice, s) != hipSuccess)
+            return HYOBFS_ERR_HIP;
+        if (obf && hipMemcpyAsync(sl.salts, b->salts + first, m * 8, hipMemcpyHostToDevice, s) != hipSuccess)
+            return HYOBFS_ERR_HIP;
+        hyobfs_batch d{};
+        d.n = m;
+        d.in = sl.in;
+        d.in_stride = b->in_stride;
+        d.in_len = b->in_len ? sl.len : nullptr;
+        d.len_uniform = b->len_uniform;
+        d.pkt_cap = b->pkt_cap;
+        d.salts = obf ? sl.salts : nullptr;
+        d.out = sl.out;
+        d.out_cap = m * b->out_stride;
+        d.out_stride = b->out_stride;
+        d.out_len = b->out_len ? sl.olen : nullptr;
+        d.workspace = sl.ws;
+        d.workspace_bytes = sl.ws_cap;
+        const int rc = run_batch(c, &d, s, obf);
+        if (rc != HYOBFS_OK) return rc;
+        if (hipMemcpyAsync(b->out + first * b->out_stride, sl.out, m * b->out_stride, hipMemcpyDeviceToHost, s) !=
+            hipSuccess)
+            return HYOBFS_ERR_HIP;
+        if (b->out_len &&
+            hipMemcpyAsync(b->out_len + first, sl.olen, m * 4, hipMemcpyDeviceToHost, s) != hipSuccess)
+            return HYOBFS_ERR_HIP;
+    }
+    for (auto& sl : c->slot)
+        if (hipStreamSynchronize(sl.s) != hipSuccess) return HYOBFS_ERR_HIP;
+    return HYOBFS_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -347,6 +451,18 @@ void hyobfs_salamander_free(hyobfs_salamander* c) {
         }
         if (c->ws) (void)hipFree(c->ws);
         if (c->stage) (void)hipHostFree(c->stage);
+        for (auto& sl : c->slot) {
+            if (sl.s) {
+                (void)hipStreamSynchronize(sl.s);
+                (void)hipStreamDestroy(sl.s);
+            }
+            (void)hipFree(sl.in);
+            (void)hipFree(sl.out);
+            (void)hipFree(sl.len);
+            (void)hipFree(sl.salts);
+            (void)hipFree(sl.olen);
+            (void)hipFree(sl.ws);
+        }
     }
     delete c;
 }
@@ -437,6 +553,24 @@ int hyobfs_salamander_obfuscate_batch(hyobfs_salamander* c, const hyobfs_batch* 
 
 int hyobfs_salamander_deobfuscate_batch(hyobfs_salamander* c, const hyobfs_batch* b, void* stream) {
     return run_batch(c, b, stream, false);
+}
+
+int hyobfs_salamander_obfuscate_host(hyobfs_salamander* c, const hyobfs_batch* b, uint64_t chunk) {
+    return run_host(c, b, chunk, true);
+}
+
+int hyobfs_salamander_deobfuscate_host(hyobfs_salamander* c, const hyobfs_batch* b, uint64_t chunk) {
+    return run_host(c, b, chunk, false);
+}
+
+void* hyobfs_host_alloc(size_t bytes) {
+    void* p = nullptr;
+    if (hipHostMalloc(&p, bytes ? bytes : 16, hipHostMallocMapped) != hipSuccess) return nullptr;
+    return p;
+}
+
+void hyobfs_host_free(void* p) {
+    if (p) (void)hipHostFree(p);
 }
 
 int hyobfs_synth_stream(uint8_t* dst, uint64_t nbytes, uint64_t seed, uint64_t start, void* stream) {

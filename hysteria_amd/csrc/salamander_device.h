@@ -373,6 +373,23 @@ __device__ __forceinline__ void chunk_contrib(const BatchParams& B, const TileBu
     }
 }
 
+// Streamed input: read exactly once.  HY_NT_LOADS=1 marks it non-temporal
+// (the hardware handles the byte misalignment either way).
+#ifndef HY_NT_LOADS
+#define HY_NT_LOADS 0
+#endif
+__device__ __forceinline__ u128 load16_stream(const uint8_t* p) {
+#if HY_NT_LOADS
+    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+    const v4u v = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(p));
+    u128 r;
+    __builtin_memcpy(&r, &v, 16);
+    return r;
+#else
+    return load16u(p);
+#endif
+}
+
 #ifndef HY_NT_STORES
 #define HY_NT_STORES 1
 #endif
@@ -437,8 +454,13 @@ struct SweepRegs {      // one sweep iteration's loads in flight
 //                  inside one payload (salt, datagram edges, sub-tile edges)
 //   prep(s+1)   -- widths, offsets (scan), salts of the next sub-tile; its 12
 //                  (or 24) BLAKE2b rounds run one per sweep iteration
+#ifdef HY_MIN_WAVES_PER_EU   // occupancy experiments: force a register budget
+#define HY_MAIN_BOUNDS __launch_bounds__(kTile, HY_MIN_WAVES_PER_EU)
+#else
+#define HY_MAIN_BOUNDS __launch_bounds__(kTile)
+#endif
 template <bool OBF, bool PACKED, int SW>
-__global__ __launch_bounds__(kTile) void salamander_kernel(BatchParams B, KeyParams K) {
+__global__ HY_MAIN_BOUNDS void salamander_kernel(BatchParams B, KeyParams K) {
     constexpr uint32_t SALT = OBF ? 8u : 0u;   // salt bytes in front of the output payload
     constexpr uint32_t SKIP = OBF ? 0u : 8u;   // salt bytes in front of the input payload
     constexpr int U = kU;
@@ -606,7 +628,7 @@ __global__ __launch_bounds__(kTile) void salamander_kernel(BatchParams B, KeyPar
                 R.v[u] = 0;
                 if (R.fast[u] && HY_OK(1, T.io[q] + (a - oq - SALT) + 16 <= B.dbg_in_bytes, T.io[q], a, oq,
                                        ((uint64_t)q << 32) | (uint32_t)s))
-                    R.v[u] = load16u(in + T.io[q] + (a - oq - SALT));
+                    R.v[u] = load16_stream(in + T.io[q] + (a - oq - SALT));
             }
         };
         auto retire = [&](uint32_t it, const SweepRegs& R) {

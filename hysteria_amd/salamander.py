@@ -65,6 +65,17 @@ def _ptr(x):
     return x.data_ptr()
 
 
+def _hptr(x):
+    """Host pointer of a numpy array / CPU torch tensor / int / None."""
+    if x is None:
+        return None
+    if isinstance(x, int):
+        return x
+    if hasattr(x, "data_ptr"):
+        return x.data_ptr()
+    return x.ctypes.data
+
+
 def _stream(stream, *tensors):
     if stream is not None:
         return stream if isinstance(stream, int) else stream.cuda_stream
@@ -180,6 +191,23 @@ class SalamanderObfuscator:
     def deobfuscate_batch(self, inp, n, *, out, **kw) -> None:
         """Deobfuscate n datagrams on the device; out_len[i] = 0 marks a dropped packet."""
         self._batch(False, inp=inp, n=n, out=out, **kw)
+
+    def _host(self, obf, *, inp, n, in_stride, out, out_stride, in_len=None, len_uniform=0, salts=None,
+              out_len=None, pkt_cap=0, chunk=0):
+        b = HyobfsBatch(n=n, in_=_hptr(inp), in_stride=in_stride, in_len=_hptr(in_len), len_uniform=len_uniform,
+                        pkt_cap=pkt_cap, salts=_hptr(salts), out=_hptr(out), out_cap=n * out_stride,
+                        out_stride=out_stride, out_len=_hptr(out_len))
+        f = self._lib.hyobfs_salamander_obfuscate_host if obf else self._lib.hyobfs_salamander_deobfuscate_host
+        check(f(self._h, ctypes.byref(b), chunk), "obfuscate_host" if obf else "deobfuscate_host")
+
+    def obfuscate_host(self, inp, n, *, in_stride, salts, out, out_stride, **kw) -> None:
+        """Obfuscate n datagrams that live in HOST memory (slotted rings, include/hyobfs.h):
+        pinned staging, H2D / kernel / D2H overlapped on three streams; synchronous."""
+        self._host(True, inp=inp, n=n, in_stride=in_stride, salts=salts, out=out, out_stride=out_stride, **kw)
+
+    def deobfuscate_host(self, inp, n, *, in_stride, out, out_stride, **kw) -> None:
+        """Deobfuscate n host-resident datagrams (out_len[i] = 0 marks a dropped one)."""
+        self._host(False, inp=inp, n=n, in_stride=in_stride, out=out, out_stride=out_stride, **kw)
 
     def keys_batch(self, salts, keys, n, stream=None) -> None:
         """keys[32*i:32*i+32] = BLAKE2b-256(PSK || salts[i]) for n device-resident salts."""

@@ -170,6 +170,29 @@ int hyobfs_salamander_obfuscate_batch(hyobfs_salamander* ctx, const hyobfs_batch
 int hyobfs_salamander_deobfuscate_batch(hyobfs_salamander* ctx, const hyobfs_batch* b,
                                         void* stream);
 
+/* ------------------------------------------------- host-resident batches */
+/*
+ * The path starts and ends in host memory (UDP socket buffers).  These calls
+ * take a hyobfs_batch whose pointers are HOST pointers, in the slotted layout
+ * of recvmmsg/sendmmsg rings: in_off == NULL (input slot i at i * in_stride),
+ * out_stride > 0 (output slot i at i * out_stride); in_len, salts, out_len
+ * are host arrays (in_len may be NULL with len_uniform).  out_off/out_total
+ * and workspace are ignored.  The batch runs in chunks of `chunk` datagrams
+ * (0 = library default) through device buffers owned by the context, on
+ * three streams, so the host-to-device copy of chunk k+1, the kernels of
+ * chunk k and the device-to-host copy of chunk k-1 overlap.  Synchronous:
+ * returns when every output byte is in host memory.  Host buffers allocated
+ * with hyobfs_host_alloc (pinned) copy at full PCIe rate; pageable memory
+ * works but is staged by the runtime.
+ */
+int hyobfs_salamander_obfuscate_host(hyobfs_salamander* ctx, const hyobfs_batch* b,
+                                     uint64_t chunk);
+int hyobfs_salamander_deobfuscate_host(hyobfs_salamander* ctx, const hyobfs_batch* b,
+                                       uint64_t chunk);
+/* pinned, device-mapped host memory (hipHostMalloc) */
+void* hyobfs_host_alloc(size_t bytes);
+void hyobfs_host_free(void* p);
+
 /* ----------------------------------------------- synthetic inputs (bench) */
 /* Device-side generators of the seeded inputs of BASELINE.md ("Synthetic
    inputs"), so large batches never cross PCIe.  SplitMix64 counter form:

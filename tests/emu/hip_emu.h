@@ -148,8 +148,9 @@ inline unsigned long long atomicCAS(unsigned long long* p, unsigned long long cm
     __atomic_compare_exchange_n(p, &cmp, v, false, __ATOMIC_RELAXED, __ATOMIC_RELAXED);
     return cmp;
 }
-enum { hipMemcpyDeviceToHost = 2 };
+enum { hipMemcpyHostToDevice = 1, hipMemcpyDeviceToHost = 2 };
 inline int hipMemcpy(void* d, const void* s, size_t n, int) { std::memcpy(d, s, n); return 0; }
+inline int hipMemcpyAsync(void* d, const void* s, size_t n, int, hipStream_t) { std::memcpy(d, s, n); return 0; }
 inline unsigned long long atomicAdd(unsigned long long* p, unsigned long long v) {
     return __atomic_fetch_add(p, v, __ATOMIC_RELAXED);
 }

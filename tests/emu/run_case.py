@@ -119,6 +119,35 @@ def case_slotted_far(n, L, stride_mb, obf):
     mm.close()
 
 
+def case_host(n, L, chunk, obf):
+    """Host-resident slotted batch through the three-slot pipeline (chunked)."""
+    rng = np.random.default_rng(n + L)
+    stride_in = L + 24
+    lens = rng.integers(0, L + 1, n).astype(np.uint32)
+    lens[:4] = [0, 8, 9, L]
+    inp = rng.integers(0, 256, n * stride_in, dtype=np.uint8)
+    salts = ref.splitmix64_array(2, 0, n)
+    out_stride = L + 8 if obf else L
+    out = np.full(n * out_stride, 0xA5, np.uint8)
+    out_len = np.zeros(n, np.uint32)
+    o = SalamanderObfuscator(b"average_password", 0)
+    if obf:
+        o.obfuscate_host(inp, n, in_stride=stride_in, in_len=lens, salts=salts, out=out, out_stride=out_stride,
+                         out_len=out_len, chunk=chunk)
+    else:
+        o.deobfuscate_host(inp, n, in_stride=stride_in, in_len=lens, out=out, out_stride=out_stride,
+                           out_len=out_len, chunk=chunk)
+    o.close()
+    for i in range(n):
+        src = inp[i * stride_in:i * stride_in + int(lens[i])].tobytes()
+        if obf:
+            exp = ref.obfuscate(b"average_password", src, int(salts[i]).to_bytes(8, "little"), out_stride)
+        else:
+            exp = ref.deobfuscate(b"average_password", src, out_stride)
+        assert int(out_len[i]) == len(exp), (i, int(out_len[i]), len(exp))
+        assert out[i * out_stride:i * out_stride + len(exp)].tobytes() == exp, i
+
+
 if __name__ == "__main__":
     lib = _lib.load()
     which = sys.argv[1]
@@ -127,6 +156,8 @@ if __name__ == "__main__":
         case_bimodal(args[0], bool(args[1]))
     elif which == "uniform":
         case_uniform(args[0], args[1], bool(args[2]))
+    elif which == "host":
+        case_host(args[0], args[1], args[2], bool(args[3]))
     elif which == "far":
         case_slotted_far(args[0], args[1], args[2], bool(args[3]))
     elif which == "ragged":

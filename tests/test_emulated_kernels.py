@@ -42,6 +42,8 @@ CASES = [
     ("ragged", "9 1500 2100 1 1", "2"),
     ("ragged", "10 1500 40 1 0", "2"),   # tiny datagrams: several per 16-byte chunk
     ("ragged", "11 1500 40 0 1", "2"),
+    ("host", "1000 300 96 1", "2"),      # host-resident batch, chunked pipeline
+    ("host", "1000 300 96 0", "2"),
     ("far", "200 300 15 1", "8"),        # workgroup bases beyond 2^31
     ("far", "200 300 15 0", "8"),
 ]

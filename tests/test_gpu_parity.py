@@ -377,3 +377,38 @@ def test_packed_output_offsets_beyond_4GiB(obfs, gpu):
         io = (int(p) * 977) % (region - L)
         exp = ref.obfuscate(PSK, h_src[io:io + L], int(h_salts[p]).to_bytes(8, "little"))
         assert got == exp, p
+
+
+@pytest.mark.parametrize("obf", [True, False])
+@pytest.mark.parametrize("pinned", [True, False])
+def test_host_batch_pipeline_vs_oracle(obfs, gpu, obf, pinned):
+    """Host-resident slotted batch (recvmmsg/sendmmsg ring shape) through the
+    H2D / kernel / D2H pipeline, chunked so several chunks cycle the 3 slots."""
+    import torch
+    n, L = 5000, 1350
+    rng = np.random.default_rng(7 + obf)
+    stride_in = 2048
+    lens = rng.integers(0, L + 1, n).astype(np.uint32)
+    lens[:4] = [0, 8, 9, L]
+    inp = rng.integers(0, 256, n * stride_in, dtype=np.uint8)
+    salts = ref.splitmix64_array(2, 0, n)
+    out_stride = 2048
+    if pinned:
+        t_in = torch.from_numpy(inp).pin_memory()
+        t_out = torch.full((n * out_stride,), 0xA5, dtype=torch.uint8).pin_memory()
+        in_buf, out_buf = t_in, t_out
+    else:
+        in_buf, out_buf = inp, np.full(n * out_stride, 0xA5, np.uint8)
+    out_len = np.zeros(n, np.uint32)
+    kw = dict(in_stride=stride_in, in_len=lens, out=out_buf, out_stride=out_stride, out_len=out_len, chunk=777)
+    if obf:
+        obfs.obfuscate_host(in_buf, n, salts=salts, **kw)
+    else:
+        obfs.deobfuscate_host(in_buf, n, **kw)
+    got = out_buf.numpy() if pinned else out_buf
+    for i in range(n):
+        src = inp[i * stride_in:i * stride_in + int(lens[i])].tobytes()
+        exp = ref.obfuscate(PSK, src, int(salts[i]).to_bytes(8, "little"), out_stride) if obf \
+            else ref.deobfuscate(PSK, src, out_stride)
+        assert int(out_len[i]) == len(exp), i
+        assert got[i * out_stride:i * out_stride + len(exp)].tobytes() == exp, i
