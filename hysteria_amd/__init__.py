@@ -3,6 +3,7 @@
 The product is ``libhyobfs.so`` (gfx950 HIP kernels behind the C ABI of
 ``include/hyobfs.h``); this package is its Python host binding.
 """
+from .conn import SalamanderPacketConn, wrap_packet_conn_salamander  # noqa: F401
 from .salamander import (  # noqa: F401
     SM_KEY_LEN,
     SM_PSK_MIN_LEN,
@@ -21,5 +22,5 @@ from .salamander import (  # noqa: F401
 __all__ = [
     "SM_KEY_LEN", "SM_PSK_MIN_LEN", "SM_SALT_LEN", "UDP_BUFFER_SIZE", "PSKTooShortError",
     "SalamanderObfuscator", "device_count", "new_salamander_obfuscator", "synth_bimodal_lengths",
-    "synth_stream", "synth_u64", "workspace_size",
+    "synth_stream", "synth_u64", "workspace_size", "SalamanderPacketConn", "wrap_packet_conn_salamander",
 ]

@@ -45,6 +45,19 @@ class HyobfsBatch(ctypes.Structure):
     ]
 
 
+class HyobfsDgram(ctypes.Structure):
+    """struct hyobfs_dgram (include/hyobfs_conn.h)."""
+
+    _fields_ = [
+        ("buf", ctypes.c_void_p),
+        ("len", ctypes.c_uint32),
+        ("cap", ctypes.c_uint32),
+        ("addr", ctypes.c_uint8 * 128),
+        ("addrlen", ctypes.c_uint32),
+        ("pad_", ctypes.c_uint32),
+    ]
+
+
 def header_functions(path: str = HEADER_PATH) -> list[str]:
     """Names of every function declared in include/*.h."""
     names = []
@@ -69,7 +82,7 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
     if not os.path.exists(path):
         raise OSError(f"{path} is missing: build it with `make -C hysteria_amd/csrc` "
                       "(or __graft_entry__.build()); there is no CPU fallback")
-    lib = ctypes.CDLL(path)
+    lib = ctypes.CDLL(path, use_errno=True)
     vp, sz, u64, u32, i32 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int
     pctx = ctypes.c_void_p
     sig = {
@@ -93,6 +106,13 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         "hyobfs_salamander_deobfuscate_host": (i32, [pctx, ctypes.POINTER(HyobfsBatch), u64]),
         "hyobfs_host_alloc": (vp, [sz]),
         "hyobfs_host_free": (None, [vp]),
+        "hyobfs_conn_wrap": (i32, [i32, pctx, u32, ctypes.POINTER(ctypes.c_void_p)]),
+        "hyobfs_conn_close": (i32, [vp]),
+        "hyobfs_conn_free": (None, [vp]),
+        "hyobfs_conn_read_from": (ctypes.c_int64, [vp, vp, sz, vp, ctypes.POINTER(u32)]),
+        "hyobfs_conn_write_to": (ctypes.c_int64, [vp, vp, sz, vp, u32]),
+        "hyobfs_conn_read_batch": (i32, [vp, vp, u32]),
+        "hyobfs_conn_write_batch": (i32, [vp, vp, u32]),
         "hyobfs_synth_stream": (i32, [vp, u64, u64, u64, vp]),
         "hyobfs_synth_u64": (i32, [vp, u64, u64, u64, vp]),
         "hyobfs_synth_bimodal_lengths": (i32, [vp, u64, u64, u64, vp]),

@@ -1,0 +1,231 @@
+// hyobfs_conn.cpp -- obfsPacketConn (extras/obfs/conn.go) over a UDP socket,
+// the Salamander work on the GPU through the C ABI of include/hyobfs.h.
+// See include/hyobfs_conn.h for the reference mapping and kept behaviour.
+#include "../../include/hyobfs_conn.h"
+
+#include <errno.h>
+#include <string.h>
+#include <sys/socket.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <mutex>
+#include <new>
+#include <vector>
+
+namespace {
+constexpr uint32_t kBuf = HYOBFS_UDP_BUFFER_SIZE;   // udpBufferSize, conn.go:10
+
+struct Ring {   // pinned, device-mapped slots of kBuf bytes
+    uint8_t* in = nullptr;
+    uint8_t* out = nullptr;
+    uint32_t* len = nullptr;
+    uint32_t* olen = nullptr;
+    uint64_t* salts = nullptr;
+    uint32_t n = 0;
+    bool alloc(uint32_t cnt) {
+        n = cnt;
+        in = static_cast<uint8_t*>(hyobfs_host_alloc((size_t)cnt * kBuf));
+        out = static_cast<uint8_t*>(hyobfs_host_alloc((size_t)cnt * kBuf));
+        len = static_cast<uint32_t*>(hyobfs_host_alloc((size_t)cnt * 4));
+        olen = static_cast<uint32_t*>(hyobfs_host_alloc((size_t)cnt * 4));
+        salts = static_cast<uint64_t*>(hyobfs_host_alloc((size_t)cnt * 8));
+        return in && out && len && olen && salts;
+    }
+    void release() {
+        hyobfs_host_free(in);
+        hyobfs_host_free(out);
+        hyobfs_host_free(len);
+        hyobfs_host_free(olen);
+        hyobfs_host_free(salts);
+        in = out = nullptr;
+        len = olen = nullptr;
+        salts = nullptr;
+    }
+};
+}  // namespace
+
+struct hyobfs_conn {
+    int fd = -1;
+    hyobfs_salamander* ctx = nullptr;
+    std::mutex read_mu, write_mu;          // readMutex / writeMutex, conn.go:25-28
+    uint8_t read_buf[kBuf];                // readBuf
+    uint8_t write_buf[kBuf];               // writeBuf
+    Ring rx, tx;
+    std::vector<mmsghdr> rmsg, wmsg;
+    std::vector<iovec> riov, wiov;
+    std::vector<sockaddr_storage> raddr;
+};
+
+extern "C" {
+
+int hyobfs_conn_wrap(int fd, hyobfs_salamander* ctx, uint32_t batch, hyobfs_conn** out) {
+    if (fd < 0 || !ctx || !out) return HYOBFS_ERR_INVALID;
+    if (batch == 0) batch = 1024;
+    auto* c = new (std::nothrow) hyobfs_conn();
+    if (!c) return HYOBFS_ERR_NOMEM;
+    c->fd = fd;
+    c->ctx = ctx;
+    if (!c->rx.alloc(batch) || !c->tx.alloc(batch)) {
+        c->rx.release();
+        c->tx.release();
+        delete c;
+        return HYOBFS_ERR_NOMEM;
+    }
+    c->rmsg.resize(batch);
+    c->wmsg.resize(batch);
+    c->riov.resize(batch);
+    c->wiov.resize(batch);
+    c->raddr.resize(batch);
+    *out = c;
+    return HYOBFS_OK;
+}
+
+void hyobfs_conn_free(hyobfs_conn* c) {
+    if (!c) return;
+    c->rx.release();
+    c->tx.release();
+    delete c;
+}
+
+int hyobfs_conn_close(hyobfs_conn* c) {   // Close(), conn.go:101-103: closes the inner conn
+    if (!c) return HYOBFS_ERR_INVALID;
+    const int rc = close(c->fd);
+    hyobfs_conn_free(c);
+    return rc == 0 ? HYOBFS_OK : HYOBFS_ERR_IO;
+}
+
+// ReadFrom, conn.go:73-88
+int64_t hyobfs_conn_read_from(hyobfs_conn* c, uint8_t* p, size_t cap, void* addr, uint32_t* addrlen) {
+    if (!c) {
+        errno = EINVAL;
+        return -1;
+    }
+    for (;;) {
+        std::lock_guard<std::mutex> lk(c->read_mu);
+        socklen_t al = addrlen ? *addrlen : 0;
+        const ssize_t n = recvfrom(c->fd, c->read_buf, kBuf, 0, static_cast<sockaddr*>(addr), addr ? &al : nullptr);
+        if (addrlen) *addrlen = al;
+        if (n <= 0) return n;   // error or empty datagram: returned as is (:77-80)
+        const size_t m = hyobfs_salamander_deobfuscate(c->ctx, c->read_buf, (size_t)n, p, cap);
+        if (m > 0) return (int64_t)m;
+        // invalid packet: drop it and read again (:86)
+    }
+}
+
+// WriteTo, conn.go:90-99
+int64_t hyobfs_conn_write_to(hyobfs_conn* c, const uint8_t* p, size_t len, const void* addr, uint32_t addrlen) {
+    if (!c) {
+        errno = EINVAL;
+        return -1;
+    }
+    std::lock_guard<std::mutex> lk(c->write_mu);
+    // Obfuscate into the 2048-byte writeBuf: 0 when len > 2040 (salamander.go:60-62)
+    const size_t nn = hyobfs_salamander_obfuscate_auto(c->ctx, p, len, c->write_buf, kBuf);
+    const ssize_t rc = sendto(c->fd, c->write_buf, nn, 0, static_cast<const sockaddr*>(addr), addrlen);
+    if (rc < 0) return -1;
+    return (int64_t)len;   // n = len(p) on success (:95-97), even for the empty-datagram case
+}
+
+int hyobfs_conn_read_batch(hyobfs_conn* c, hyobfs_dgram* msgs, uint32_t n) {
+    if (!c || (!msgs && n)) {
+        errno = EINVAL;
+        return -1;
+    }
+    if (n == 0) return 0;
+    std::lock_guard<std::mutex> lk(c->read_mu);
+    n = std::min(n, c->rx.n);
+    for (;;) {
+        for (uint32_t i = 0; i < n; ++i) {
+            c->riov[i].iov_base = c->rx.in + (size_t)i * kBuf;
+            c->riov[i].iov_len = kBuf;
+            memset(&c->rmsg[i], 0, sizeof(mmsghdr));
+            c->rmsg[i].msg_hdr.msg_iov = &c->riov[i];
+            c->rmsg[i].msg_hdr.msg_iovlen = 1;
+            c->rmsg[i].msg_hdr.msg_name = &c->raddr[i];
+            c->rmsg[i].msg_hdr.msg_namelen = sizeof(sockaddr_storage);
+        }
+        const int k = recvmmsg(c->fd, c->rmsg.data(), n, MSG_WAITFORONE, nullptr);
+        if (k <= 0) return k;
+        for (int i = 0; i < k; ++i) c->rx.len[i] = c->rmsg[i].msg_len;
+        hyobfs_batch b{};
+        b.n = (uint64_t)k;
+        b.in = c->rx.in;
+        b.in_stride = kBuf;
+        b.in_len = c->rx.len;
+        b.out = c->rx.out;
+        b.out_stride = kBuf;
+        b.out_cap = (uint64_t)k * kBuf;
+        b.out_len = c->rx.olen;
+        if (hyobfs_salamander_deobfuscate_host(c->ctx, &b, 0) != HYOBFS_OK) {
+            errno = EIO;
+            return -1;
+        }
+        int got = 0;
+        for (int i = 0; i < k; ++i) {
+            const uint32_t m = c->rx.olen[i];
+            if (m == 0 || m > msgs[got].cap) continue;   // Deobfuscate returned 0: dropped
+            memcpy(msgs[got].buf, c->rx.out + (size_t)i * kBuf, m);
+            msgs[got].len = m;
+            const uint32_t al = std::min<uint32_t>(c->rmsg[i].msg_hdr.msg_namelen, sizeof msgs[got].addr);
+            memcpy(msgs[got].addr, &c->raddr[i], al);
+            msgs[got].addrlen = al;
+            ++got;
+        }
+        if (got) return got;
+        // every datagram was invalid: read again, like ReadFrom
+    }
+}
+
+int hyobfs_conn_write_batch(hyobfs_conn* c, const hyobfs_dgram* msgs, uint32_t n) {
+    if (!c || (!msgs && n)) {
+        errno = EINVAL;
+        return -1;
+    }
+    std::lock_guard<std::mutex> lk(c->write_mu);
+    uint32_t sent = 0;
+    while (sent < n) {
+        const uint32_t k = std::min(n - sent, c->tx.n);
+        for (uint32_t i = 0; i < k; ++i) {
+            const hyobfs_dgram& d = msgs[sent + i];
+            const uint32_t L = std::min<uint32_t>(d.len, kBuf);   // longer ones are dropped below anyway
+            memcpy(c->tx.in + (size_t)i * kBuf, d.buf, L);
+            c->tx.len[i] = d.len > kBuf ? kBuf : d.len;   // > 2040 -> out_len 0 -> empty datagram
+        }
+        hyobfs_salamander_next_salts(c->ctx, reinterpret_cast<uint8_t*>(c->tx.salts), k);   // RandSrc
+        hyobfs_batch b{};
+        b.n = k;
+        b.in = c->tx.in;
+        b.in_stride = kBuf;
+        b.in_len = c->tx.len;
+        b.salts = c->tx.salts;
+        b.out = c->tx.out;
+        b.out_stride = kBuf;   // len(writeBuf): Obfuscate needs len+8 <= 2048
+        b.out_cap = (uint64_t)k * kBuf;
+        b.out_len = c->tx.olen;
+        if (hyobfs_salamander_obfuscate_host(c->ctx, &b, 0) != HYOBFS_OK) {
+            errno = EIO;
+            return -1;
+        }
+        for (uint32_t i = 0; i < k; ++i) {
+            const hyobfs_dgram& d = msgs[sent + i];
+            c->wiov[i].iov_base = c->tx.out + (size_t)i * kBuf;
+            c->wiov[i].iov_len = c->tx.olen[i];
+            memset(&c->wmsg[i], 0, sizeof(mmsghdr));
+            c->wmsg[i].msg_hdr.msg_iov = &c->wiov[i];
+            c->wmsg[i].msg_hdr.msg_iovlen = 1;
+            c->wmsg[i].msg_hdr.msg_name = const_cast<uint8_t*>(d.addr);
+            c->wmsg[i].msg_hdr.msg_namelen = d.addrlen;
+        }
+        uint32_t done = 0;
+        while (done < k) {
+            const int r = sendmmsg(c->fd, c->wmsg.data() + done, k - done, 0);
+            if (r < 0) return sent + done ? (int)(sent + done) : -1;
+            done += (uint32_t)r;
+        }
+        sent += k;
+    }
+    return (int)sent;
+}
+
+}  // extern "C"

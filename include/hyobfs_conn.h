@@ -1,0 +1,77 @@
+/*
+ * hyobfs_conn.h -- obfsPacketConn (apernet/hysteria extras/obfs/conn.go) over
+ * a UDP socket, with the Salamander work on the GPU (include/hyobfs.h).
+ *
+ *   Go (reference)                                     C ABI
+ *   -------------------------------------------------  ---------------------------------
+ *   WrapPacketConnSalamander(conn, psk)  salamander.go:51-57
+ *     + wrapPacketConn(conn, ob)         conn.go:56-71  hyobfs_conn_wrap(fd, ctx, ...)
+ *   (*obfsPacketConn).ReadFrom(p)        conn.go:73-88  hyobfs_conn_read_from
+ *   (*obfsPacketConn).WriteTo(p, addr)   conn.go:90-99  hyobfs_conn_write_to
+ *   (*obfsPacketConn).Close()            conn.go:101-103 hyobfs_conn_close
+ *   LocalAddr / deadlines / Set*Buffer   conn.go:105-133 the caller keeps the fd
+ *   (new) batched receive / send                        hyobfs_conn_read_batch / _write_batch
+ *
+ * Reference behaviour kept:
+ *   - ReadFrom drops datagrams that do not deobfuscate (len <= 8 or larger than
+ *     the caller's buffer) and reads again; a socket error or an empty read
+ *     is returned as is (conn.go:77-86).
+ *   - WriteTo obfuscates into a 2048-byte buffer (udpBufferSize, conn.go:10); a
+ *     payload longer than 2040 bytes makes Obfuscate return 0, the wrapper then
+ *     sends an EMPTY datagram and still reports len(p) (conn.go:92-98).
+ *   - one read and one write may run concurrently (readMutex/writeMutex).
+ * Batched calls move up to `batch` datagrams per recvmmsg/sendmmsg and one GPU
+ * batch (pinned rings owned by the connection).
+ */
+#ifndef HYOBFS_CONN_H
+#define HYOBFS_CONN_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "hyobfs.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* udpBufferSize, conn.go:10: receive/send buffer per datagram */
+#define HYOBFS_UDP_BUFFER_SIZE 2048
+
+typedef struct hyobfs_conn hyobfs_conn;
+
+/* one datagram of a batched call; addr is a struct sockaddr_storage */
+typedef struct hyobfs_dgram {
+    uint8_t* buf;       /* payload (read: destination, write: source) */
+    uint32_t len;       /* write: payload length; read: bytes received */
+    uint32_t cap;       /* read: capacity of buf */
+    uint8_t addr[128];  /* struct sockaddr_storage */
+    uint32_t addrlen;
+    uint32_t pad_;
+} hyobfs_dgram;
+
+/* Wrap a bound UDP socket.  The connection does not own ctx.  batch = the
+   largest number of datagrams per batched call (0 = 1024). */
+int hyobfs_conn_wrap(int fd, hyobfs_salamander* ctx, uint32_t batch, hyobfs_conn** out);
+/* Close(): closes the socket and frees the connection. */
+int hyobfs_conn_close(hyobfs_conn* c);
+/* frees the connection, leaves the socket open */
+void hyobfs_conn_free(hyobfs_conn* c);
+
+/* ReadFrom: bytes written to p (>= 0), or -1 with errno set (socket error). */
+int64_t hyobfs_conn_read_from(hyobfs_conn* c, uint8_t* p, size_t cap, void* addr, uint32_t* addrlen);
+/* WriteTo: len on success (also for the empty-datagram quirk), -1 with errno set. */
+int64_t hyobfs_conn_write_to(hyobfs_conn* c, const uint8_t* p, size_t len, const void* addr,
+                             uint32_t addrlen);
+/* Receive up to n valid datagrams (blocks for the first; invalid ones, and
+   empty datagrams that ReadFrom would return as a 0-byte read, are dropped).
+   Returns the count (>= 0), or -1 with errno set. */
+int hyobfs_conn_read_batch(hyobfs_conn* c, hyobfs_dgram* msgs, uint32_t n);
+/* Obfuscate and send n datagrams with one GPU batch.  Returns the count sent,
+   or -1 with errno set. */
+int hyobfs_conn_write_batch(hyobfs_conn* c, const hyobfs_dgram* msgs, uint32_t n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HYOBFS_CONN_H */

@@ -1,0 +1,144 @@
+"""Loopback-UDP scenarios for SalamanderPacketConn (extras/obfs/conn.go semantics).
+
+Shared by the CPU-emulated tier (tests/emu/run_case.py conn) and the GPU tier
+(tests/test_gpu_parity.py).  Wire bytes are checked against the oracle
+(oracle/salamander_ref.py); the reference's own conn behaviour being checked is
+cited per step.
+"""
+import socket
+
+import numpy as np
+
+from hysteria_amd.conn import SalamanderPacketConn
+from hysteria_amd.salamander import SalamanderObfuscator
+from oracle import salamander_ref as ref
+
+PSK = b"conn_test_password"
+
+
+def _udp():
+    s = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
+    s.bind(("127.0.0.1", 0))
+    s.settimeout(10.0)
+    return s
+
+
+def _payload(rng, n):
+    return rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+
+
+def run_conn_scenarios(device: int = 0, batch: int = 64, n_batch: int = 200):
+    rng = np.random.default_rng(7)
+    sa, sb, raw = _udp(), _udp(), _udp()
+    oa, ob = SalamanderObfuscator(PSK, device), SalamanderObfuscator(PSK, device)
+    oa.seed(11)
+    ca, cb = SalamanderPacketConn(sa, oa, batch=batch), SalamanderPacketConn(sb, ob, batch=batch)
+    a_addr, b_addr, r_addr = ca.local_addr(), cb.local_addr(), raw.getsockname()
+    try:
+        # WriteTo -> ReadFrom round trip (conn.go:73-99)
+        for n in (1, 9, 100, 1200, 2040):
+            p = _payload(rng, n)
+            assert ca.write_to(p, b_addr) == n
+            got, addr = cb.read_from()
+            assert got == p and addr == a_addr, n
+
+        # wire bytes = salt || p ^ BLAKE2b-256(PSK||salt) (salamander.go:59-72)
+        for n in (0, 1, 31, 32, 33, 1350, 2040):
+            p = _payload(rng, n)
+            ca.write_to(p, r_addr)
+            wire, addr = raw.recvfrom(4096)
+            assert addr == a_addr and len(wire) == n + 8
+            assert wire == ref.obfuscate(PSK, p, wire[:8], n + 8), n
+
+        # a zero-length payload goes out as an 8-byte datagram, which Deobfuscate
+        # rejects (len <= 8, salamander.go:75-77): the reader drops it and reads on
+        ca.write_to(b"", b_addr)
+        mark = _payload(rng, 77)
+        ca.write_to(mark, b_addr)
+        assert cb.read_from()[0] == mark
+
+        # > 2040 bytes: Obfuscate returns 0 and WriteTo sends an EMPTY datagram,
+        # still reporting len(p) (conn.go:92-98) ...
+        big = _payload(rng, 2041)
+        assert ca.write_to(big, r_addr) == 2041
+        wire, _ = raw.recvfrom(4096)
+        assert wire == b""
+        # ... and ReadFrom returns an empty read for it (n <= 0 branch, conn.go:77-80)
+        assert ca.write_to(big, b_addr) == 2041
+        got, addr = cb.read_from()
+        assert got == b"" and addr == a_addr
+
+        # invalid datagrams are dropped and the read goes on (conn.go:86)
+        raw.sendto(b"12345", b_addr)
+        raw.sendto(b"12345678", b_addr)
+        p = _payload(rng, 200)
+        raw.sendto(ref.obfuscate(PSK, p, b"\x01" * 8, 208), b_addr)   # too big for a 100-byte buffer
+        q = _payload(rng, 60)
+        raw.sendto(ref.obfuscate(PSK, q, b"\x02" * 8, 68), b_addr)
+        got, addr = cb.read_from(100)
+        assert got == q and addr == r_addr
+        # a datagram from the oracle side deobfuscates on the GPU side
+        raw.sendto(ref.obfuscate(PSK, p, b"saltsalt", 208), b_addr)
+        assert cb.read_from()[0] == p
+
+        # batched: WriteBatch -> oracle on the wire
+        lens = [int(x) for x in rng.integers(0, 2100, n_batch)]
+        lens[:4] = [0, 2040, 2041, 9]
+        pays = [_payload(rng, n) for n in lens]
+        sent = 0
+        for i in range(0, n_batch, 32):   # stay inside the loopback socket buffer
+            grp = pays[i:i + 32]
+            sent += ca.write_batch([(p, r_addr) for p in grp])
+            for p in grp:
+                wire, addr = raw.recvfrom(4096)
+                assert addr == a_addr
+                if len(p) > 2040:
+                    assert wire == b""
+                else:
+                    assert wire == ref.obfuscate(PSK, p, wire[:8], len(p) + 8)
+        assert sent == n_batch
+
+        # batched: WriteBatch -> ReadBatch; invalid and empty datagrams are dropped
+        expect = [p for p in pays if 1 <= len(p) <= 2040]
+        got = []
+        for i in range(0, n_batch, 32):
+            grp = pays[i:i + 32]
+            assert ca.write_batch([(p, b_addr) for p in grp]) == len(grp)
+            raw.sendto(b"x" * 8, b_addr)   # junk between groups
+            want = sum(1 for p in grp if 1 <= len(p) <= 2040)
+            have = 0
+            while have < want:
+                msgs = cb.read_batch(64)
+                for m, addr in msgs:
+                    assert addr == a_addr
+                got.extend(m for m, _ in msgs)
+                have += len(msgs)
+        assert got == expect
+
+        # ReadBatch takes oracle-made datagrams too
+        qs = [_payload(rng, int(n)) for n in rng.integers(9, 1500, 20)]
+        for j, q in enumerate(qs):
+            raw.sendto(ref.obfuscate(PSK, q, bytes([j]) * 8, len(q) + 8), b_addr)
+        got = []
+        while len(got) < len(qs):
+            got += [m for m, _ in cb.read_batch(64)]
+        assert got == qs
+
+        # SetReadDeadline: an idle read times out
+        cb.settimeout(0.2)
+        try:
+            cb.read_from()
+            raise AssertionError("read did not time out")
+        except TimeoutError:
+            pass
+        try:
+            cb.read_batch(8)
+            raise AssertionError("read_batch did not time out")
+        except TimeoutError:
+            pass
+    finally:
+        ca.close()
+        cb.close()
+        raw.close()
+        oa.close()
+        ob.close()

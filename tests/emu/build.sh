@@ -9,6 +9,7 @@ FLAGS="${EMU_EXTRA:-} -std=c++20 -O1 -g -fPIC -DHYOBFS_EMULATE -I. -I$SRC -x c++
 mkdir -p build
 $CXX $FLAGS -c $SRC/salamander.hip -o build/salamander.o &
 $CXX $FLAGS -c $SRC/hyobfs_api.cpp -o build/hyobfs_api.o &
+$CXX $FLAGS -c $SRC/hyobfs_conn.cpp -o build/hyobfs_conn.o &
 for n in $(seq 0 15); do $CXX $FLAGS -DHY_SW=$n -c $SRC/salamander_inst.hip -o build/inst_sw$n.o & done
 wait
 $CXX -shared -fsanitize=address -pthread -o ${EMU_OUT:-libhyobfs_emu.so} build/*.o

@@ -13,7 +13,8 @@
 // per-wave slot array between two barriers of the 64 lanes.  __shared__
 // variables are function-local statics (one workgroup at a time).  All lanes
 // are assumed active at every wavefront operation, which the kernels satisfy
-// (they only shuffle in wave-uniform code).
+// (they only shuffle in wave-uniform code).  Launches from several host
+// threads are serialised.
 #pragma once
 #include <algorithm>
 #include <atomic>
@@ -22,6 +23,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <memory>
+#include <mutex>
 #include <thread>
 #include <vector>
 
@@ -80,8 +82,11 @@ inline T xchg(T v, int src_lane) {
     return out;
 }
 
+inline std::mutex g_launch_mu;   // the state above is global: one launch at a time
+
 template <class F>
 inline void launch(dim3 grid, dim3 block, F&& body) {
+    std::lock_guard<std::mutex> lk(g_launch_mu);
     g_grid = grid;
     g_blockdim = block;
     const uint32_t nt = block.x;

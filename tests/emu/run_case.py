@@ -158,6 +158,10 @@ if __name__ == "__main__":
         case_uniform(args[0], args[1], bool(args[2]))
     elif which == "host":
         case_host(args[0], args[1], args[2], bool(args[3]))
+    elif which == "conn":
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        from conn_cases import run_conn_scenarios
+        run_conn_scenarios(batch=args[0], n_batch=args[1])
     elif which == "far":
         case_slotted_far(args[0], args[1], args[2], bool(args[3]))
     elif which == "ragged":

@@ -44,6 +44,7 @@ CASES = [
     ("ragged", "11 1500 40 0 1", "2"),
     ("host", "1000 300 96 1", "2"),      # host-resident batch, chunked pipeline
     ("host", "1000 300 96 0", "2"),
+    ("conn", "64 120", "2"),             # UDP loopback through the conn wrapper (conn.go)
     ("far", "200 300 15 1", "8"),        # workgroup bases beyond 2^31
     ("far", "200 300 15 0", "8"),
 ]

@@ -412,3 +412,11 @@ def test_host_batch_pipeline_vs_oracle(obfs, gpu, obf, pinned):
             else ref.deobfuscate(PSK, src, out_stride)
         assert int(out_len[i]) == len(exp), i
         assert got[i * out_stride:i * out_stride + len(exp)].tobytes() == exp, i
+
+
+@pytest.mark.gpu
+def test_packet_conn_loopback(gpu):
+    """obfsPacketConn (conn.go:73-99) over loopback UDP: ReadFrom/WriteTo quirks,
+    batched recvmmsg/sendmmsg paths, wire bytes against the oracle."""
+    from conn_cases import run_conn_scenarios
+    run_conn_scenarios(device=0, batch=1024, n_batch=400)

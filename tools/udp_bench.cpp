@@ -1,0 +1,215 @@
+// udp_bench -- host-to-host rate of the Salamander PacketConn wrapper
+// (BASELINE config 5): loopback UDP, sender conns obfuscate with
+// hyobfs_conn_write_batch (sendmmsg + one GPU batch), receiver conns
+// deobfuscate with hyobfs_conn_read_batch (recvmmsg + one GPU batch).
+// Every received payload is checked (sequence number + content tag).
+//
+//   udp_bench [mode=batch|single|raw] [pairs=4] [seconds=5] [len=1200] [batch=1024]
+//
+// "raw" sends and receives the same datagrams with plain sendmmsg/recvmmsg and no
+// obfuscation: the loopback socket ceiling.  "single" uses WriteTo/ReadFrom, one
+// GPU round trip per datagram, the shape of the reference's obfsPacketConn.
+// Prints one JSON line.
+#include <arpa/inet.h>
+#include <netinet/in.h>
+#include <string.h>
+#include <sys/socket.h>
+#include <unistd.h>
+
+#include <atomic>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../include/hyobfs_conn.h"
+
+static uint64_t tag(uint64_t seq) { return seq * 0x9E3779B97F4A7C15ull ^ 0xD1B54A32D192ED03ull; }
+
+static void fill(uint8_t* p, uint32_t len, uint64_t seq) {
+    memcpy(p, &seq, 8);
+    const uint64_t t = tag(seq);
+    for (uint32_t o = 8; o + 8 <= len; o += 8) memcpy(p + o, &t, 8);
+}
+
+static bool check(const uint8_t* p, uint32_t len, uint32_t want_len) {
+    if (len != want_len) return false;
+    uint64_t seq;
+    memcpy(&seq, p, 8);
+    const uint64_t t = tag(seq);
+    for (uint32_t o = 8; o + 8 <= len; o += 8)
+        if (memcmp(p + o, &t, 8) != 0) return false;
+    return true;
+}
+
+static int udp_socket(sockaddr_in* bound) {
+    int fd = socket(AF_INET, SOCK_DGRAM, 0);
+    int big = 64 << 20;
+    setsockopt(fd, SOL_SOCKET, SO_RCVBUF, &big, sizeof big);
+    setsockopt(fd, SOL_SOCKET, SO_SNDBUF, &big, sizeof big);
+    sockaddr_in a{};
+    a.sin_family = AF_INET;
+    a.sin_addr.s_addr = htonl(INADDR_LOOPBACK);
+    if (bind(fd, reinterpret_cast<sockaddr*>(&a), sizeof a) != 0) {
+        perror("bind");
+        exit(1);
+    }
+    socklen_t al = sizeof *bound;
+    getsockname(fd, reinterpret_cast<sockaddr*>(bound), &al);
+    timeval tv{0, 200000};
+    setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof tv);
+    return fd;
+}
+
+struct Pair {
+    int sfd = -1, rfd = -1;
+    sockaddr_in saddr{}, raddr{};
+    hyobfs_salamander* sctx = nullptr;
+    hyobfs_salamander* rctx = nullptr;
+    hyobfs_conn* sc = nullptr;
+    hyobfs_conn* rc = nullptr;
+    std::atomic<uint64_t> sent{0}, recvd{0}, bad{0}, calls{0};
+};
+
+int main(int argc, char** argv) {
+    const std::string mode = argc > 1 ? argv[1] : "batch";
+    const int pairs = argc > 2 ? atoi(argv[2]) : 4;
+    const double seconds = argc > 3 ? atof(argv[3]) : 5.0;
+    const uint32_t len = argc > 4 ? (uint32_t)atoi(argv[4]) : 1200;
+    const uint32_t batch = argc > 5 ? (uint32_t)atoi(argv[5]) : 1024;
+    const uint8_t psk[] = "udp_bench_password";
+    const bool raw = mode == "raw", single = mode == "single";
+    if (len < 16 || len > 2040) {
+        fprintf(stderr, "len must be in [16, 2040]\n");
+        return 2;
+    }
+
+    std::vector<Pair> P(pairs);
+    for (auto& p : P) {
+        p.sfd = udp_socket(&p.saddr);
+        p.rfd = udp_socket(&p.raddr);
+        if (!raw) {
+            int st = hyobfs_salamander_new(psk, sizeof psk - 1, 0, &p.sctx);
+            if (st == HYOBFS_OK) st = hyobfs_salamander_new(psk, sizeof psk - 1, 0, &p.rctx);
+            if (st == HYOBFS_OK) st = hyobfs_conn_wrap(p.sfd, p.sctx, batch, &p.sc);
+            if (st == HYOBFS_OK) st = hyobfs_conn_wrap(p.rfd, p.rctx, batch, &p.rc);
+            if (st != HYOBFS_OK) {
+                fprintf(stderr, "setup: %s\n", hyobfs_status_string(st));
+                return 1;
+            }
+        }
+    }
+
+    std::atomic<bool> stop{false}, rstop{false};
+    std::vector<std::thread> th;
+    for (int pi = 0; pi < pairs; ++pi) {
+        Pair& p = P[pi];
+        th.emplace_back([&, pi] {   // sender
+            std::vector<uint8_t> buf((size_t)batch * len);
+            std::vector<hyobfs_dgram> d(batch);
+            std::vector<mmsghdr> mh(batch);
+            std::vector<iovec> iov(batch);
+            for (uint32_t i = 0; i < batch; ++i) {
+                d[i].buf = buf.data() + (size_t)i * len;
+                d[i].len = len;
+                memcpy(d[i].addr, &p.raddr, sizeof p.raddr);
+                d[i].addrlen = sizeof p.raddr;
+                iov[i] = {d[i].buf, len};
+                memset(&mh[i], 0, sizeof mh[i]);
+                mh[i].msg_hdr.msg_iov = &iov[i];
+                mh[i].msg_hdr.msg_iovlen = 1;
+                mh[i].msg_hdr.msg_name = &p.raddr;
+                mh[i].msg_hdr.msg_namelen = sizeof p.raddr;
+            }
+            uint64_t seq = (uint64_t)pi << 48;
+            while (!stop.load(std::memory_order_relaxed)) {
+                for (uint32_t i = 0; i < batch; ++i) fill(d[i].buf, len, seq++);
+                if (single) {
+                    for (uint32_t i = 0; i < batch && !stop.load(std::memory_order_relaxed); ++i) {
+                        if (hyobfs_conn_write_to(p.sc, d[i].buf, len, &p.raddr, sizeof p.raddr) > 0) p.sent++;
+                    }
+                } else if (raw) {
+                    uint32_t done = 0;
+                    while (done < batch) {
+                        int r = sendmmsg(p.sfd, mh.data() + done, batch - done, 0);
+                        if (r <= 0) break;
+                        done += r;
+                    }
+                    p.sent += done;
+                } else {
+                    int r = hyobfs_conn_write_batch(p.sc, d.data(), batch);
+                    if (r > 0) p.sent += r;
+                }
+            }
+        });
+        th.emplace_back([&] {   // receiver
+            std::vector<uint8_t> buf((size_t)batch * 2048);
+            std::vector<hyobfs_dgram> d(batch);
+            std::vector<mmsghdr> mh(batch);
+            std::vector<iovec> iov(batch);
+            for (uint32_t i = 0; i < batch; ++i) {
+                d[i].buf = buf.data() + (size_t)i * 2048;
+                d[i].cap = 2048;
+                iov[i] = {d[i].buf, 2048};
+            }
+            while (!rstop.load(std::memory_order_relaxed)) {
+                int k;
+                if (single) {
+                    int64_t n = hyobfs_conn_read_from(p.rc, d[0].buf, 2048, nullptr, nullptr);
+                    k = n > 0 ? 1 : 0;
+                    d[0].len = n > 0 ? (uint32_t)n : 0;
+                } else if (raw) {
+                    for (uint32_t i = 0; i < batch; ++i) {
+                        memset(&mh[i], 0, sizeof mh[i]);
+                        mh[i].msg_hdr.msg_iov = &iov[i];
+                        mh[i].msg_hdr.msg_iovlen = 1;
+                    }
+                    k = recvmmsg(p.rfd, mh.data(), batch, MSG_WAITFORONE, nullptr);
+                    for (int i = 0; i < k; ++i) d[i].len = mh[i].msg_len;
+                } else {
+                    k = hyobfs_conn_read_batch(p.rc, d.data(), batch);
+                }
+                if (k <= 0) continue;
+                p.calls++;
+                uint64_t bad = 0;
+                for (int i = 0; i < k; ++i) bad += !check(d[i].buf, d[i].len, len);
+                p.recvd += k;
+                p.bad += bad;
+            }
+        });
+    }
+
+    // warm up 0.5 s, then count over the timed window
+    std::this_thread::sleep_for(std::chrono::milliseconds(500));
+    uint64_t r0 = 0, s0 = 0;
+    for (auto& p : P) r0 += p.recvd, s0 += p.sent;
+    const auto t0 = std::chrono::steady_clock::now();
+    std::this_thread::sleep_for(std::chrono::duration<double>(seconds));
+    uint64_t r1 = 0, s1 = 0;
+    for (auto& p : P) r1 += p.recvd, s1 += p.sent;
+    const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    stop = true;
+    std::this_thread::sleep_for(std::chrono::milliseconds(400));
+    rstop = true;
+    for (auto& t : th) t.join();
+    uint64_t bad = 0, calls = 0, sent = 0, recvd = 0;
+    for (auto& p : P) {
+        bad += p.bad, calls += p.calls, sent += p.sent, recvd += p.recvd;
+        if (p.sc) hyobfs_conn_free(p.sc);
+        if (p.rc) hyobfs_conn_free(p.rc);
+        close(p.sfd);
+        close(p.rfd);
+        hyobfs_salamander_free(p.sctx);
+        hyobfs_salamander_free(p.rctx);
+    }
+    const double rx = (double)(r1 - r0), tx = (double)(s1 - s0);
+    printf("{\"mode\": \"%s\", \"pairs\": %d, \"len\": %u, \"batch\": %u, \"seconds\": %.3f, "
+           "\"rx_datagrams_per_s\": %.0f, \"tx_datagrams_per_s\": %.0f, \"rx_payload_GiB_s\": %.4f, "
+           "\"tx_payload_GiB_s\": %.4f, \"loss_frac\": %.4f, \"bad\": %llu, \"avg_per_read\": %.1f}\n",
+           mode.c_str(), pairs, len, batch, dt, rx / dt, tx / dt, rx * len / dt / (1u << 30), tx * len / dt / (1u << 30),
+           sent ? 1.0 - (double)recvd / (double)sent : 0.0, (unsigned long long)bad,
+           calls ? (double)recvd / (double)calls : 0.0);
+    return bad ? 1 : 0;
+}
