@@ -231,7 +231,8 @@ def main():
         torch.cuda.synchronize()
         parity = {"roundtrip_identity": bool(torch.equal(back[:payload_bytes], inp[:payload_bytes]))}
 
-    total_payload = payload_bytes * world
+    # wall_* cover all K timed steps: every step processes the whole batch once
+    total_payload = payload_bytes * world * args.steps
     value = total_payload / wall_obf / 2**30
     achieved = obf_bytes / ev_obf / 1e9
     res = {

@@ -12,7 +12,7 @@ if [[ $MODE == *calib* || $MODE == all ]]; then
   step calib 180 ./tools/hbm_copy > "$OUT/hbm_copy.json"
 fi
 if [[ $MODE == *test* || $MODE == all ]]; then
-  step pytest 700 python -m pytest tests -x -v -m gpu > "$OUT/pytest_gpu.log" 2>&1
+  step pytest 700 python -u -m pytest tests -x -v -m gpu --timeout 120 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1
 fi
 if [[ $MODE == *bench* || $MODE == all ]]; then
   step bench 300 python bench.py --steps 20 --warmup 5 --cpu-seconds 6 > "$OUT/bench.json" 2> "$OUT/bench.err"
