@@ -251,7 +251,8 @@ def main():
         "config": config,
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                     "kernel": "salamander_kernel<obfuscate>",
+                     "kernel": ("salamander_wave_kernel<obfuscate, slotted>" if args.workload == "uniform"
+                                else "salamander_kernel<obfuscate, packed> (+ tile-sum scan)"),
                      "algorithmic_bytes_per_launch": obf_bytes, "avg_launch_ms": round(ev_obf * 1e3, 4)},
         "deobfuscate": {"value": round(total_payload / wall_deobf / 2**30, 2), "unit": "GiB/s",
                         "ms_per_step": round(wall_deobf / args.steps * 1e3, 4),

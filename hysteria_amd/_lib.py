@@ -92,6 +92,7 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         "hyobfs_salamander_new": (i32, [vp, sz, i32, ctypes.POINTER(ctypes.c_void_p)]),
         "hyobfs_salamander_free": (None, [pctx]),
         "hyobfs_salamander_device": (i32, [pctx]),
+        "hyobfs_salamander_set_kernel": (i32, [pctx, i32]),
         "hyobfs_salamander_seed": (None, [pctx, u64]),
         "hyobfs_salamander_next_salts": (None, [pctx, vp, sz]),
         "hyobfs_salamander_key": (i32, [pctx, vp, vp]),

@@ -33,6 +33,7 @@ struct hyobfs_salamander {
     hipStream_t stream = nullptr;
     std::mutex mu;              // per-packet path, salt source, owned buffers (lk)
     uint64_t rng = 0;           // SplitMix64 state (RandSrc)
+    int kernel = 0;             // HYOBFS_KERNEL_* for batch launches
     // per-packet staging in mapped pinned host memory: [in | out | salt | len | total]
     uint8_t* stage = nullptr;
     uint8_t* stage_dev = nullptr;
@@ -208,6 +209,7 @@ size_t run_one(hyobfs_salamander* c, bool obf, const uint8_t* in, size_t in_len,
     uint32_t* h_len = reinterpret_cast<uint32_t*>(h_misc + 8);
     *h_len = 0xFFFFFFFFu;
     BatchParams b{};
+    b.kernel = c->kernel;
     b.n = 1;
     b.in = c->stage_dev;
     b.len_uniform = (uint32_t)in_len;
@@ -248,6 +250,7 @@ int validate_and_fill(hyobfs_salamander* c, const hyobfs_batch* b, bool obf, Bat
     bp.out_off = b->out_off;
     bp.out_len = b->out_len;
     bp.out_total = reinterpret_cast<unsigned long long*>(b->out_total);
+    bp.kernel = c->kernel;
     if (b->out_total && hipMemsetAsync(b->out_total, 0, sizeof(uint64_t), s) != hipSuccess)
         return HYOBFS_ERR_HIP;
     if (b->n && b->out_stride == 0) {   // packed: tile-sum scratch
@@ -468,6 +471,12 @@ void hyobfs_salamander_free(hyobfs_salamander* c) {
 }
 
 int hyobfs_salamander_device(const hyobfs_salamander* c) { return c ? c->device : -1; }
+
+int hyobfs_salamander_set_kernel(hyobfs_salamander* c, int kernel) {
+    if (!c || kernel < HYOBFS_KERNEL_AUTO || kernel > HYOBFS_KERNEL_PERSISTENT) return HYOBFS_ERR_INVALID;
+    c->kernel = kernel;
+    return HYOBFS_OK;
+}
 
 void hyobfs_salamander_seed(hyobfs_salamander* c, uint64_t seed) {
     if (!c) return;

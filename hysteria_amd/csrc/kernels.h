@@ -7,8 +7,24 @@
 #include <hip/hip_runtime.h>
 #endif
 #include <stdint.h>
+#include <cstdlib>
+#include <cstring>
 
 namespace hyobfs {
+
+// Orders one wave's LDS writes before its later LDS reads by other lanes of the
+// same wave.  A wave's LDS instructions execute in order, so this only has to
+// stop the compiler from moving memory operations across it (wavefront-scope
+// fences emit no instruction).
+#ifdef HYOBFS_EMULATE
+inline void hy_wave_sync() { hyemu_wave_sync(); }
+#else
+__device__ __forceinline__ void hy_wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+#endif
 
 constexpr int kTile = 256;          // datagrams per workgroup tile (= threads)
 constexpr uint32_t kMaxDatagram = (1u << 24) - 64;  // longest datagram a batch accepts
@@ -47,6 +63,8 @@ struct BatchParams {
     uint64_t* tile_sums;          // packed: scratch, ntiles+1 entries
     uint64_t part_len;            // main kernel: n / grid datagrams per workgroup ...
     uint64_t part_rem;            // ... plus one for the first n % grid workgroups
+    uint32_t run_log2;            // wave kernel: datagrams per run = 2^run_log2
+    int kernel;                   // HYOBFS_KERNEL_* of the context (0 = auto)
     // HY_BOUNDS_CHECK builds only (build_variants/, never the shipped library):
     // first out-of-range access recorded here instead of performed
     unsigned long long* dbg;

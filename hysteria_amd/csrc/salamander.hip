@@ -18,7 +18,7 @@
 // store; the few chunks at datagram edges are finished by their owning lane.
 // No MFMA: there is no contraction; the kernel is HBM-bound (2L+16 bytes per
 // obfuscated datagram).
-#include "salamander_device.h"
+#include "salamander_wave.h"
 
 namespace hyobfs {
 
@@ -27,7 +27,11 @@ namespace hyobfs {
     extern template void launch_main_sw<true, true, n>(const BatchParams&, const KeyParams&, hipStream_t);  \
     extern template void launch_main_sw<true, false, n>(const BatchParams&, const KeyParams&, hipStream_t); \
     extern template void launch_main_sw<false, true, n>(const BatchParams&, const KeyParams&, hipStream_t); \
-    extern template void launch_main_sw<false, false, n>(const BatchParams&, const KeyParams&, hipStream_t);
+    extern template void launch_main_sw<false, false, n>(const BatchParams&, const KeyParams&, hipStream_t); \
+    extern template void launch_wave_sw<true, true, n>(const BatchParams&, const KeyParams&, hipStream_t);  \
+    extern template void launch_wave_sw<true, false, n>(const BatchParams&, const KeyParams&, hipStream_t); \
+    extern template void launch_wave_sw<false, true, n>(const BatchParams&, const KeyParams&, hipStream_t); \
+    extern template void launch_wave_sw<false, false, n>(const BatchParams&, const KeyParams&, hipStream_t);
 HY_EXTERN_SW(0) HY_EXTERN_SW(1) HY_EXTERN_SW(2) HY_EXTERN_SW(3) HY_EXTERN_SW(4) HY_EXTERN_SW(5)
 HY_EXTERN_SW(6) HY_EXTERN_SW(7) HY_EXTERN_SW(8) HY_EXTERN_SW(9) HY_EXTERN_SW(10) HY_EXTERN_SW(11)
 HY_EXTERN_SW(12) HY_EXTERN_SW(13) HY_EXTERN_SW(14) HY_EXTERN_SW(15)
@@ -133,14 +137,34 @@ __global__ void synth_bimodal_kernel(uint32_t* dst, uint64_t n, uint64_t seed, u
 
 // ------------------------------------------------------------------ launchers
 
+// Kernel choice per layout ("Kernels"): slotted batches run the
+// wave-group kernel (salamander_wave.h), packed batches the persistent
+// workgroup kernel (salamander_device.h), which handles the boundary-heavy
+// ragged mixes better.  HYOBFS_KERNEL=wave|persistent forces one.
+static int kernel_override() {
+    static int v = -2;
+    if (v == -2) {
+        const char* e = std::getenv("HYOBFS_KERNEL");
+        v = !e ? -1 : std::strcmp(e, "wave") == 0 ? 1 : std::strcmp(e, "persistent") == 0 ? 0 : -1;
+    }
+    return v;
+}
+
 template <bool OBF, bool PACKED>
 static void launch_main(const BatchParams& bp, const KeyParams& k, hipStream_t s) {
+    const int ov = bp.kernel ? (bp.kernel == 1 ? 1 : 0) : kernel_override();
+    const bool wave = ov >= 0 ? ov == 1 : !PACKED;
     switch (k.salt_pos >> 3) {
-#define HY_CASE(n) \
-    case n: launch_main_sw<OBF, PACKED, n>(bp, k, s); break;
+#define HY_CASE(n)                                    \
+    case n:                                           \
+        if (wave)                                     \
+            launch_wave_sw<OBF, PACKED, n>(bp, k, s); \
+        else                                          \
+            launch_main_sw<OBF, PACKED, n>(bp, k, s); \
+        break;
         HY_CASE(0) HY_CASE(1) HY_CASE(2) HY_CASE(3) HY_CASE(4) HY_CASE(5) HY_CASE(6) HY_CASE(7)
         HY_CASE(8) HY_CASE(9) HY_CASE(10) HY_CASE(11) HY_CASE(12) HY_CASE(13) HY_CASE(14)
-        default: launch_main_sw<OBF, PACKED, 15>(bp, k, s); break;
+        HY_CASE(15)
 #undef HY_CASE
     }
 }

@@ -1,6 +1,6 @@
 // salamander_inst.hip -- instantiates the main kernel for one salt word
 // (compiled once per HY_SW = 0..15, see Makefile).
-#include "salamander_device.h"
+#include "salamander_wave.h"
 
 #ifndef HY_SW
 #error "compile with -DHY_SW=<salt word 0..15>"
@@ -11,4 +11,8 @@ template void launch_main_sw<true, true, HY_SW>(const BatchParams&, const KeyPar
 template void launch_main_sw<true, false, HY_SW>(const BatchParams&, const KeyParams&, hipStream_t);
 template void launch_main_sw<false, true, HY_SW>(const BatchParams&, const KeyParams&, hipStream_t);
 template void launch_main_sw<false, false, HY_SW>(const BatchParams&, const KeyParams&, hipStream_t);
+template void launch_wave_sw<true, true, HY_SW>(const BatchParams&, const KeyParams&, hipStream_t);
+template void launch_wave_sw<true, false, HY_SW>(const BatchParams&, const KeyParams&, hipStream_t);
+template void launch_wave_sw<false, true, HY_SW>(const BatchParams&, const KeyParams&, hipStream_t);
+template void launch_wave_sw<false, false, HY_SW>(const BatchParams&, const KeyParams&, hipStream_t);
 }  // namespace hyobfs

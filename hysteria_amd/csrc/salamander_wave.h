@@ -1,0 +1,369 @@
+// salamander_wave.h -- the wave-group Salamander kernel (gfx950).
+//
+// One wavefront owns a GROUP of 64 consecutive datagrams (lane l <-> datagram
+// l) and does everything for it without workgroup barriers:
+//   1. metadata: length, input offset, salt, output width and offset (packed
+//      layout: wavefront scan on top of the tile prefix), drop rules
+//      (salamander.go:60-62, :75-77);
+//   2. key = BLAKE2b-256(PSK || salt) (salamander.go:88-91), all 12 (or 24)
+//      rounds in registers, rotated to the output's 32-byte phase, into LDS;
+//   3. sweep: the group's output bytes are one contiguous range; the 64 lanes
+//      walk it in 16-byte chunks, 1 KiB per wave instruction, kWU chunks per
+//      lane in flight.  A chunk inside one payload is one unaligned 16 B load,
+//      one LDS key read, four XORs and one aligned non-temporal 16 B store;
+//   4. boundary: lane l finishes the chunks datagram l owns that are not inside
+//      one payload (salt bytes, datagram and group edges) with masked stores.
+// The four waves of a workgroup are independent (their LDS slices are
+// separate), so a CU holds up to 32 waves at different phases: the VALU-bound
+// hash of one wave runs while the others stream.  The register budget (64
+// VGPRs, 8 waves per SIMD) is what the design is for: the bytes in flight
+// per CU come from wave count, not from a deep per-wave pipeline.
+#pragma once
+#include "salamander_device.h"
+
+namespace hyobfs {
+
+constexpr int kGroup = 64;           // datagrams per wave group (= lanes)
+constexpr int kWavesPerBlock = 4;    // independent waves per workgroup
+#ifndef HY_WU
+#define HY_WU 8
+#endif
+constexpr int kWU = HY_WU;           // chunks per lane per sweep iteration
+#ifndef HY_RUN_LOG2
+#define HY_RUN_LOG2 3
+#endif
+#ifndef HY_WAVE_MIN_WAVES
+#define HY_WAVE_MIN_WAVES 8          // __launch_bounds__ min waves per SIMD
+#endif
+
+struct GroupBuf {                    // one wave's group, in LDS
+    uint2 ow[kGroup];                // output region start (relative to base), width (0 = dropped)
+    uint32_t pe[kGroup];             // max region end over earlier datagrams of the group
+    uint64_t io[kGroup];             // input payload start (absolute byte offset)
+    uint64_t salt[kGroup];           // salt (obfuscate)
+    uint64_t delta[kGroup];          // real output offset - virtual offset (the run's)
+    uint4 key[2 * kGroup];           // key rotated to the output's 32-byte phase, 2 halves
+};
+
+// ---- BLAKE2b message words of the device block(s).  The message is
+// PSK || salt, zero padded: every word after the salt's is a compile-time 0,
+// the words before it are PSK words (wave-uniform, scalar), the salt's one or
+// two words are per lane.  (KeyParams: hyobfs_api.cpp make_key_params.)
+template <int SW, int BLK>
+__device__ __forceinline__ uint64_t wmsg(const KeyParams& K, uint64_t lo, uint64_t hi, int idx) {
+    if (BLK == 1) return idx == 0 ? hi : 0ull;   // second block: the salt's tail only
+    if (idx < SW) return K.m[idx];
+    if (idx == SW) return K.m[idx] | lo;
+    if (idx == SW + 1) return hi;
+    return 0ull;
+}
+
+template <int R, int SW, int BLK>
+__device__ __forceinline__ void wround(uint64_t v[16], const KeyParams& K, uint64_t lo, uint64_t hi) {
+#define HY_W(k) wmsg<SW, BLK>(K, lo, hi, kSigma[R][k])
+    HY_G(v, 0, 4, 8, 12, HY_W(0), HY_W(1));
+    HY_G(v, 1, 5, 9, 13, HY_W(2), HY_W(3));
+    HY_G(v, 2, 6, 10, 14, HY_W(4), HY_W(5));
+    HY_G(v, 3, 7, 11, 15, HY_W(6), HY_W(7));
+    HY_G(v, 0, 5, 10, 15, HY_W(8), HY_W(9));
+    HY_G(v, 1, 6, 11, 12, HY_W(10), HY_W(11));
+    HY_G(v, 2, 7, 8, 13, HY_W(12), HY_W(13));
+    HY_G(v, 3, 4, 9, 14, HY_W(14), HY_W(15));
+#undef HY_W
+}
+
+template <int SW, int BLK>
+__device__ __forceinline__ void wrounds(uint64_t v[16], const KeyParams& K, uint64_t lo, uint64_t hi) {
+    wround<0, SW, BLK>(v, K, lo, hi);
+    wround<1, SW, BLK>(v, K, lo, hi);
+    wround<2, SW, BLK>(v, K, lo, hi);
+    wround<3, SW, BLK>(v, K, lo, hi);
+    wround<4, SW, BLK>(v, K, lo, hi);
+    wround<5, SW, BLK>(v, K, lo, hi);
+    wround<6, SW, BLK>(v, K, lo, hi);
+    wround<7, SW, BLK>(v, K, lo, hi);
+    wround<8, SW, BLK>(v, K, lo, hi);
+    wround<9, SW, BLK>(v, K, lo, hi);
+    wround<10, SW, BLK>(v, K, lo, hi);
+    wround<11, SW, BLK>(v, K, lo, hi);
+}
+
+// keyLocked (salamander.go:88-91) for one lane's salt: BLAKE2b-256 of
+// PSK || salt from the host's PSK-only prefix state (RFC 7693 F, unrolled).
+template <int SW>
+__device__ __forceinline__ void wave_key(const KeyParams& K, uint64_t salt, uint64_t key[4]) {
+    const uint32_t sb = (K.salt_pos & 7) * 8;
+    const uint64_t lo = salt << sb;
+    const uint64_t hi = sb ? (salt >> (64 - sb)) : 0ull;
+    uint64_t v[16];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        v[i] = K.h[i];
+        v[i + 8] = kIV[i];
+    }
+    v[12] ^= K.t[0];
+    v[14] = (K.nblk == 1) ? ~v[14] : v[14];
+    wrounds<SW, 0>(v, K, lo, hi);
+    if (SW == 15 && K.nblk == 2) {   // salt_pos 121..127: chain into the salt's second block
+        uint64_t h1[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) h1[i] = K.h[i] ^ v[i] ^ v[i + 8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            v[i] = h1[i];
+            v[i + 8] = kIV[i];
+        }
+        v[12] ^= K.t[1];
+        v[14] = ~v[14];
+        wrounds<SW, 1>(v, K, lo, hi);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) key[i] = h1[i] ^ v[i] ^ v[i + 8];
+        return;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) key[i] = K.h[i] ^ v[i] ^ v[i + 8];
+}
+
+// All bytes datagram k of the group contributes to the 16-byte chunk at relative a.
+template <bool OBF>
+__device__ __forceinline__ void group_contrib(const GroupBuf& G, const uint8_t* __restrict__ in, uint32_t k,
+                                              uint32_t a, u128& r, uint32_t& cov) {
+    constexpr uint32_t SALT = OBF ? 8u : 0u;
+    const uint2 owk = G.ow[k];
+    const uint32_t oq = owk.x, wq = owk.y;
+    if (wq == 0 || oq + wq <= a || oq >= a + 16) return;
+    if (OBF) {   // salt bytes [oq, oq + 8)
+        const uint32_t sb = max(oq, a), se = min(oq + 8u, a + 16u);
+        if (sb < se) {
+            u128 S = (u128)G.salt[k];
+            S = oq >= a ? (S << (8 * (oq - a))) : (S >> (8 * (a - oq)));
+            r |= S & bytemask(sb - a, se - a);
+            cov |= ((1u << (se - sb)) - 1u) << (sb - a);
+        }
+    }
+    const uint32_t op = oq + SALT, pend = oq + wq;
+    const uint32_t ps = max(op, a), pe = min(pend, a + 16u);
+    if (ps < pe) {
+        const uint32_t PL = wq - SALT;
+        const int base = (int)a - (int)op;   // payload index of chunk byte 0
+        const uint8_t* src = in + G.io[k];
+        u128 X = 0;
+        if (PL >= 16) {   // one 16-byte window inside the payload, shifted into place
+            const int ws = min(max(base, 0), (int)PL - 16);
+            const u128 V = load16u(src + ws);
+            const int d = ws - base;
+            X = d >= 0 ? (V << (8 * d)) : (V >> (8 * -d));
+        } else {
+            for (uint32_t j = ps - a; j < pe - a; ++j) X |= (u128)src[base + (int)j] << (8 * j);
+        }
+        const uint4 kk = G.key[2 * k + ((a >> 4) & 1)];
+        u128 k128;
+        __builtin_memcpy(&k128, &kk, 16);
+        r |= (X ^ k128) & bytemask(ps - a, pe - a);
+        cov |= ((1u << (pe - ps)) - 1u) << (ps - a);
+    }
+}
+
+// Streamed input of the wave kernel: read once, non-temporal (measured faster
+// here; the persistent kernel keeps HY_NT_LOADS).
+__device__ __forceinline__ u128 load16_nt(const uint8_t* p) {
+#ifdef HYOBFS_EMULATE
+    return load16u(p);
+#else
+    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+    const v4u v = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(p));
+    u128 r;
+    __builtin_memcpy(&r, &v, 16);
+    return r;
+#endif
+}
+
+// Last datagram of the group whose region starts at or before virtual offset a.
+__device__ __forceinline__ uint32_t group_search(const GroupBuf& G, uint32_t a) {
+    uint32_t qq = 0;   // last datagram whose region starts at or before a
+#pragma unroll
+    for (uint32_t step = kGroup / 2; step; step >>= 1) qq = (G.ow[qq + step].x <= a) ? qq + step : qq;
+    return qq;
+}
+
+template <bool OBF, bool PACKED, int SW>
+__global__ __launch_bounds__(kGroup* kWavesPerBlock, HY_WAVE_MIN_WAVES) void salamander_wave_kernel(BatchParams B,
+                                                                                                    KeyParams K) {
+    constexpr uint32_t SALT = OBF ? 8u : 0u;   // salt bytes in front of the output payload
+    constexpr uint32_t SKIP = OBF ? 0u : 8u;   // salt bytes in front of the input payload
+    constexpr int U = kWU;
+    __shared__ GroupBuf gbuf[kWavesPerBlock];
+
+    const int lane = threadIdx.x & 63;
+    const uint32_t wid = uni32(threadIdx.x >> 6);
+    GroupBuf& G = gbuf[wid];
+    const uint8_t* __restrict__ in = B.in;
+    // Runs of RUN = 2^rl consecutive datagrams; wave w owns runs w, w + Wt,
+    // w + 2 Wt, ... (64 / RUN of them), so the waves running at one time work
+    // on neighbouring runs and the chip sweeps memory in address order.
+    const uint32_t rl = B.run_log2, RUN = 1u << rl;
+    const uint64_t Wt = (uint64_t)gridDim.x * kWavesPerBlock;
+    const uint64_t w = (uint64_t)blockIdx.x * kWavesPerBlock + wid;
+    const uint32_t j = (uint32_t)lane >> rl, i = (uint32_t)lane & (RUN - 1);
+    const uint64_t r = (uint64_t)j * Wt + w;   // this lane's run
+    const uint64_t p = (r << rl) + i;          // this lane's datagram
+    const bool live = p < B.n;
+    const uint32_t cnt = uni32((uint32_t)wave_sum(live ? 1u : 0u));   // live lanes are a prefix
+    if (cnt == 0) return;
+
+    // ---- 1. metadata
+    uint32_t L = 0;
+    uint64_t ioff = 0, salt = 0;
+    if (live) {
+        L = pkt_len(B, p);
+        ioff = pkt_in_off(B, p);
+        if (OBF) salt = B.salts[p];
+    }
+    uint32_t W = live ? out_width<OBF>(L, B.pkt_cap) : 0u;
+    uint64_t ooff, rfirst;   // output offset of the datagram / of its run's first datagram
+    if (PACKED) {   // (RUN = 64) tile prefix + widths of the tile's earlier datagrams + wave scan
+        const uint64_t p0 = w * kGroup;
+        const uint64_t tb = p0 / kTile * kTile;
+        uint32_t pre = 0;
+        for (uint64_t q = tb + lane; q < p0; q += kGroup) pre += out_width<OBF>(pkt_len(B, q), B.pkt_cap);
+        rfirst = uni64(B.tile_prefix[p0 / kTile] + wave_sum(pre));
+        ooff = rfirst + wave_incl_scan(W, lane) - W;
+    } else {
+        ooff = p * B.out_stride;
+        rfirst = (r << rl) * B.out_stride;
+    }
+    if (W && ooff + W > B.out_cap) W = 0;   // does not fit: dropped, offsets unchanged
+    if (live) {
+        if (B.out_off) B.out_off[p] = ooff;
+        if (B.out_len) B.out_len[p] = W;
+    }
+    if (B.out_total) {   // bytes this wave writes
+        const uint64_t written = uni64(wave_sum(W));
+        if (lane == 0 && written) atomicAdd(B.out_total, (unsigned long long)written);
+    }
+    if (!OBF && W) salt = load8u(in + ioff);   // the wire's salt
+
+    // ---- virtual layout: the wave's runs back to back, each from its
+    // 16-aligned real base; real address = virtual + delta (a multiple of 16)
+    const uint64_t rb = rfirst & ~15ull;
+    uint64_t rend = W ? ooff + W : rb;   // end of the run's written bytes
+    for (uint32_t m = 1; m < RUN; m <<= 1) rend = max(rend, (uint64_t)__shfl_xor(rend, (int)m, 64));
+    const uint32_t nch = live ? (uint32_t)((rend - rb + 15) >> 4) : 0u;   // the run's chunks
+    const uint32_t vp = (uint32_t)wave_incl_scan(i == 0 ? nch : 0u, lane) - (i == 0 ? nch : 0u);
+    const uint32_t vrun = __shfl(vp, (int)(lane & ~(RUN - 1)), 64) << 4;   // run's virtual start
+    const uint32_t rel = live ? vrun + (uint32_t)min<uint64_t>(ooff - rb, (uint64_t)nch << 4) : 0xFFFFFFFFu;
+    const uint32_t end = W ? rel + W : 0u;
+    uint32_t incm = end;   // inclusive max-scan of region ends (chunk ownership)
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(incm, d, 64);
+        if (lane >= d) incm = max(incm, y);
+    }
+    const uint32_t pe = __shfl_up(incm, 1, 64);
+    const uint32_t totm = uni32(__shfl(incm, 63, 64));
+    // metadata to LDS first: only salt and rel stay live through the hash
+    G.ow[lane] = make_uint2(rel, W);
+    G.pe[lane] = lane ? pe : 0u;
+    G.io[lane] = ioff + SKIP;
+    G.delta[lane] = rb - vrun;
+    if (OBF) G.salt[lane] = salt;
+
+    // ---- 2. key, rotated to the output phase
+    {
+        uint64_t key[4], kr[4];
+#ifdef HY_X_NOHASH   // ablation builds only (timing experiments; wrong output)
+        key[0] = salt; key[1] = salt * 3; key[2] = salt ^ 7; key[3] = salt + 1;
+#else
+        wave_key<SW>(K, salt, key);
+#endif
+        rotl_key_bytes(key, (rel + SALT) & 31u, kr);
+        G.key[2 * lane] = make_uint4((uint32_t)kr[0], (uint32_t)(kr[0] >> 32), (uint32_t)kr[1],
+                                     (uint32_t)(kr[1] >> 32));
+        G.key[2 * lane + 1] = make_uint4((uint32_t)kr[2], (uint32_t)(kr[2] >> 32), (uint32_t)kr[3],
+                                         (uint32_t)(kr[3] >> 32));
+    }
+    hy_wave_sync();
+
+    // ---- 3. sweep: virtual chunks inside one payload.  (Finishing the
+    // boundary chunks here instead, so that whole 128-byte lines leave in one
+    // wave instruction, measured slower: the divergent byte merging costs
+    // more than the partial-line write-backs it saves.)
+    const uint32_t nchunks = (totm + 15u) >> 4;
+    for (uint32_t c0 = 0; c0 < nchunks; c0 += kGroup * U) {
+        u128 v[U];
+        uint32_t q[U];
+        bool fast[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t c = c0 + u * kGroup + lane;
+            const uint32_t a = c << 4;
+            const uint32_t qq = group_search(G, a);
+            q[u] = qq;
+            const uint2 owq = G.ow[qq];
+            fast[u] = (c < nchunks) && owq.y != 0 && owq.x + SALT <= a && a + 16 <= owq.x + owq.y;
+            v[u] = 0;
+            if (fast[u]) v[u] = load16_nt(in + G.io[qq] + (a - owq.x - SALT));
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (!fast[u]) continue;
+            const uint32_t a = (c0 + u * kGroup + lane) << 4;
+            const uint4 kk = G.key[2 * q[u] + ((a >> 4) & 1)];
+            u128 k128;
+            __builtin_memcpy(&k128, &kk, 16);
+            store16_stream(B.out + (G.delta[q[u]] + a), v[u] ^ k128);
+        }
+    }
+
+    // ---- 4. boundary: chunks datagram `lane` owns that are not inside one payload
+    const uint2 own = G.ow[lane];
+#ifdef HY_X_NOBOUND   // ablation builds only (timing experiments; wrong output)
+    if (false) {
+#else
+    if (own.y) {
+#endif
+        const uint32_t st = own.x, en = own.x + own.y;
+        const uint32_t cs = st >> 4, ce = (en - 1) >> 4;
+        const bool own_cs = G.pe[lane] <= (cs << 4);
+        const uint32_t cand[3] = {cs, cs + 1, ce};
+        const bool use[3] = {own_cs, cs + 1 <= ce, ce > cs + 1};
+        uint8_t* outb = B.out + G.delta[lane];   // a chunk's contributors share its run
+#pragma unroll
+        for (int t = 0; t < 3; ++t) {
+            if (!use[t]) continue;
+            const uint32_t a = cand[t] << 4;
+            if (st + SALT <= a && a + 16 <= en) continue;   // inside the payload: swept
+            u128 rr = 0;
+            uint32_t cov = 0;
+            for (uint32_t k = lane; k < cnt && G.ow[k].x < a + 16; ++k) group_contrib<OBF>(G, in, k, a, rr, cov);
+            if (cov) store_masked(outb + a, rr, cov);
+        }
+    }
+}
+
+// Datagrams per run for slotted batches (HYOBFS_RUN_LOG2 overrides).  3 = runs
+// of 8 datagrams, ~9.6 KB at 1200 B: small enough that the waves in flight
+// sweep a ~80 MB window in address order (whole 64-datagram groups leave a
+// ~630 MB window, tools/region_copy.hip), large enough that few 128-byte
+// lines are shared between runs of different waves.
+inline uint32_t wave_run_log2() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = std::getenv("HYOBFS_RUN_LOG2");
+        v = e ? std::atoi(e) : HY_RUN_LOG2;
+        v = v < 0 ? 0 : v > 6 ? 6 : v;
+    }
+    return (uint32_t)v;
+}
+
+template <bool OBF, bool PACKED, int SW>
+void launch_wave_sw(const BatchParams& bp, const KeyParams& k, hipStream_t s) {
+    const uint64_t ngroups = div_up(bp.n, kGroup);
+    const uint64_t blocks = div_up(ngroups, kWavesPerBlock);
+    BatchParams b = bp;
+    b.run_log2 = PACKED ? 6u : wave_run_log2();
+    hipLaunchKernelGGL((salamander_wave_kernel<OBF, PACKED, SW>), dim3((uint32_t)blocks),
+                       dim3(kGroup * kWavesPerBlock), 0, s, b, k);
+}
+
+}  // namespace hyobfs

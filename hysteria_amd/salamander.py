@@ -123,6 +123,12 @@ class SalamanderObfuscator:
     def __exit__(self, *exc):
         self.close()
 
+    KERNELS = {"auto": 0, "wave": 1, "persistent": 2}
+
+    def set_kernel(self, kernel: str) -> None:
+        """Batch kernel of this context: "auto" (per layout), "wave" or "persistent"."""
+        check(self._lib.hyobfs_salamander_set_kernel(self._h, self.KERNELS[kernel]), "set_kernel")
+
     # ------------------------------------------------------------ salt source
     def seed(self, seed: int) -> None:
         """Make the salt source deterministic (the reference's RandSrc, salamander.go:29)."""

@@ -89,6 +89,13 @@ int hyobfs_salamander_new(const uint8_t* psk, size_t psk_len, int device,
 void hyobfs_salamander_free(hyobfs_salamander* ctx);
 int hyobfs_salamander_device(const hyobfs_salamander* ctx);
 
+/* Batch kernel of this context (no reference counterpart: a tuning knob).
+   HYOBFS_KERNEL_AUTO picks per layout (slotted -> wave-group kernel, packed ->
+   persistent kernel; the HYOBFS_KERNEL environment variable overrides AUTO).
+   Returns HYOBFS_ERR_INVALID for an unknown value.  Outputs are identical. */
+enum { HYOBFS_KERNEL_AUTO = 0, HYOBFS_KERNEL_WAVE = 1, HYOBFS_KERNEL_PERSISTENT = 2 };
+int hyobfs_salamander_set_kernel(hyobfs_salamander* ctx, int kernel);
+
 /* Salt source (the reference's RandSrc, salamander.go:29,43,65).  The context
    seeds itself from the clock at creation like the reference; _seed makes it
    deterministic.  _next_salts writes n salts (8 bytes each, in host memory). */

@@ -8,7 +8,7 @@ def per_dispatch(counter):
     vals = {}
     for f in glob.glob(os.path.join(root, f"pmc_{counter}", "run_counter_collection.csv")):
         for row in csv.DictReader(open(f)):
-            if "salamander_kernel<true" not in row["Kernel_Name"] or row["Counter_Name"] != counter:
+            if not ("salamander_kernel<true" in row["Kernel_Name"] or "salamander_wave_kernel<true" in row["Kernel_Name"]) or row["Counter_Name"] != counter:
                 continue
             vals[row["Dispatch_Id"]] = vals.get(row["Dispatch_Id"], 0.0) + float(row["Counter_Value"])
     v = sorted(vals.values())

@@ -41,6 +41,10 @@ struct dim3 {
 struct uint4 {
     uint32_t x, y, z, w;
 };
+struct uint2 {
+    uint32_t x, y;
+};
+inline uint2 make_uint2(uint32_t a, uint32_t b) { return uint2{a, b}; }
 inline uint4 make_uint4(uint32_t a, uint32_t b, uint32_t c, uint32_t d) { return uint4{a, b, c, d}; }
 
 typedef int hipError_t;
@@ -82,6 +86,8 @@ inline T xchg(T v, int src_lane) {
     return out;
 }
 
+inline void wave_sync() { g_ctx.wave[(int)t_thread.x >> 6]->arrive_and_wait(); }
+
 inline std::mutex g_launch_mu;   // the state above is global: one launch at a time
 
 template <class F>
@@ -116,6 +122,7 @@ inline void launch(dim3 grid, dim3 block, F&& body) {
 #define gridDim (hyemu::g_grid)
 #define blockDim (hyemu::g_blockdim)
 
+inline void hyemu_wave_sync() { hyemu::wave_sync(); }
 inline void __syncthreads() { hyemu::g_ctx.block->arrive_and_wait(); }
 
 template <class T>

@@ -50,6 +50,42 @@ CASES = [
 ]
 
 
+# The wave kernel (forced for packed layouts too) and its run length (datagrams per run = 2^run_log2, salamander_wave.h):
+# single-datagram runs, short runs and whole 64-datagram groups, on ragged
+# slotted and packed layouts with tiny datagrams, gaps and zero widths.
+RUN_CASES = [
+    ("ragged", "9 1500 2100 1 1", "0"),
+    ("ragged", "11 1500 40 0 1", "0"),
+    ("ragged", "12 700 100 1 0", "1"),
+    ("ragged", "13 700 30 0 0", "3"),
+    ("ragged", "14 700 200 0 1", "3"),
+    ("ragged", "15 700 19 1 1", "6"),
+    ("uniform", "300 1200 1", "6"),
+    ("uniform", "300 1200 0", "0"),
+]
+
+
+def _run(emu_lib, which, args, extra_env):
+    env = dict(os.environ, HYOBFS_LIB=emu_lib, LD_PRELOAD=_asan_runtime(), ASAN_OPTIONS="detect_leaks=0",
+               **extra_env)
+    r = subprocess.run([sys.executable, os.path.join(EMU, "run_case.py"), which] + args.split(), env=env,
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0 and "ok" in r.stdout, (r.stdout[-2000:], r.stderr[-4000:])
+
+
+@pytest.mark.parametrize("which,args,run_log2", RUN_CASES)
+def test_emulated_wave_kernel_run_lengths(emu_lib, which, args, run_log2):
+    _run(emu_lib, which, args, {"HYOBFS_RUN_LOG2": run_log2, "HYOBFS_KERNEL": "wave"})
+
+
+@pytest.mark.parametrize("which,args,cus", CASES)
+def test_emulated_persistent_kernel(emu_lib, which, args, cus):
+    """The persistent workgroup kernel (HYOBFS_KERNEL=persistent) on the same cases."""
+    if which in ("conn", "host"):
+        pytest.skip("kernel-independent host paths run once, under the default kernel")
+    _run(emu_lib, which, args, {"HYEMU_CUS": cus, "HYOBFS_KERNEL": "persistent"})
+
+
 @pytest.mark.parametrize("which,args,cus", CASES)
 def test_emulated_kernel_vs_oracle(emu_lib, which, args, cus):
     env = dict(os.environ, HYOBFS_LIB=emu_lib, LD_PRELOAD=_asan_runtime(), ASAN_OPTIONS="detect_leaks=0",

@@ -17,10 +17,13 @@ pytestmark = pytest.mark.gpu
 PSK = b"average_password"
 
 
-@pytest.fixture(scope="module")
-def obfs(gpu):
+@pytest.fixture(scope="module", params=["auto", "wave", "persistent"])
+def obfs(gpu, request):
+    """One context per batch kernel: auto (the shipped per-layout choice), and
+    each kernel forced on every layout (salamander_wave.h, salamander_device.h)."""
     import hysteria_amd
     o = hysteria_amd.SalamanderObfuscator(PSK, 0)
+    o.set_kernel(request.param)
     yield o
     o.close()
 
