@@ -32,6 +32,9 @@ constexpr int kWU = HY_WU;           // chunks per lane per sweep iteration
 #ifndef HY_RUN_LOG2
 #define HY_RUN_LOG2 3
 #endif
+#ifndef HY_PREFETCH
+#define HY_PREFETCH 0                // 1: software-pipelined sweep (two register sets)
+#endif
 #ifndef HY_WAVE_MIN_WAVES
 #define HY_WAVE_MIN_WAVES 8          // __launch_bounds__ min waves per SIMD
 #endif
@@ -289,31 +292,54 @@ __global__ __launch_bounds__(kGroup* kWavesPerBlock, HY_WAVE_MIN_WAVES) void sal
     // wave instruction, measured slower: the divergent byte merging costs
     // more than the partial-line write-backs it saves.)
     const uint32_t nchunks = (totm + 15u) >> 4;
-    for (uint32_t c0 = 0; c0 < nchunks; c0 += kGroup * U) {
+    struct Sweep {   // one iteration's loads in flight
         u128 v[U];
         uint32_t q[U];
         bool fast[U];
+    };
+    auto issue = [&](uint32_t c0, Sweep& R) {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const uint32_t c = c0 + u * kGroup + lane;
             const uint32_t a = c << 4;
             const uint32_t qq = group_search(G, a);
-            q[u] = qq;
+            R.q[u] = qq;
             const uint2 owq = G.ow[qq];
-            fast[u] = (c < nchunks) && owq.y != 0 && owq.x + SALT <= a && a + 16 <= owq.x + owq.y;
-            v[u] = 0;
-            if (fast[u]) v[u] = load16_nt(in + G.io[qq] + (a - owq.x - SALT));
+            R.fast[u] = (c < nchunks) && owq.y != 0 && owq.x + SALT <= a && a + 16 <= owq.x + owq.y;
+            R.v[u] = 0;
+            if (R.fast[u]) R.v[u] = load16_nt(in + G.io[qq] + (a - owq.x - SALT));
         }
+    };
+    auto retire = [&](uint32_t c0, const Sweep& R) {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            if (!fast[u]) continue;
+            if (!R.fast[u]) continue;
             const uint32_t a = (c0 + u * kGroup + lane) << 4;
-            const uint4 kk = G.key[2 * q[u] + ((a >> 4) & 1)];
+            const uint4 kk = G.key[2 * R.q[u] + ((a >> 4) & 1)];
             u128 k128;
             __builtin_memcpy(&k128, &kk, 16);
-            store16_stream(B.out + (G.delta[q[u]] + a), v[u] ^ k128);
+            store16_stream(B.out + (G.delta[R.q[u]] + a), R.v[u] ^ k128);
         }
+    };
+    constexpr uint32_t STEP = kGroup * U;
+#if HY_PREFETCH
+    // two register sets: iteration i+1's loads are in flight while i retires
+    Sweep RA, RB;
+    if (nchunks) issue(0, RA);
+    for (uint32_t c0 = 0; c0 < nchunks; c0 += 2 * STEP) {
+        const bool h1 = c0 + STEP < nchunks, h2 = c0 + 2 * STEP < nchunks;
+        if (h1) issue(c0 + STEP, RB);
+        retire(c0, RA);
+        if (h2) issue(c0 + 2 * STEP, RA);
+        if (h1) retire(c0 + STEP, RB);
     }
+#else
+    for (uint32_t c0 = 0; c0 < nchunks; c0 += STEP) {
+        Sweep R;
+        issue(c0, R);
+        retire(c0, R);
+    }
+#endif
 
     // ---- 4. boundary: chunks datagram `lane` owns that are not inside one payload
     const uint2 own = G.ow[lane];
