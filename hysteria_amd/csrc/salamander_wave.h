@@ -7,12 +7,18 @@
 //      (salamander.go:60-62, :75-77);
 //   2. key = BLAKE2b-256(PSK || salt) (salamander.go:88-91), all 12 (or 24)
 //      rounds in registers, rotated to the output's 32-byte phase, into LDS;
-//   3. sweep: the group's output bytes are one contiguous range; the 64 lanes
+//   3. boundary: lane l computes the chunks datagram l owns that are not
+//      inside one payload (salt bytes, datagram and run edges) and parks the
+//      complete ones in LDS, pre-XORed with its key half;
+//   4. sweep: the group's output bytes are one contiguous range; the 64 lanes
 //      walk it in 16-byte chunks, 1 KiB per wave instruction, kWU chunks per
 //      lane in flight.  A chunk inside one payload is one unaligned 16 B load,
-//      one LDS key read, four XORs and one aligned non-temporal 16 B store;
-//   4. boundary: lane l finishes the chunks datagram l owns that are not inside
-//      one payload (salt bytes, datagram and group edges) with masked stores.
+//      one LDS key read, four XORs and one aligned non-temporal 16 B store; a
+//      parked chunk is an LDS read instead of the load, so every byte of a
+//      128-byte line leaves in the same store instructions (no partial-line
+//      write-backs);
+//   5. late: the few boundary chunks that were not parked (partial chunks at
+//      gaps and run edges, slot overflow) are stored with byte masks.
 // The four waves of a workgroup are independent (their LDS slices are
 // separate), so a CU holds up to 32 waves at different phases: the VALU-bound
 // hash of one wave runs while the others stream.  The register budget (64
@@ -39,13 +45,16 @@ constexpr int kWU = HY_WU;           // chunks per lane per sweep iteration
 #define HY_WAVE_MIN_WAVES 8          // __launch_bounds__ min waves per SIMD
 #endif
 
-struct GroupBuf {                    // one wave's group, in LDS
-    uint2 ow[kGroup];                // output region start (relative to base), width (0 = dropped)
-    uint32_t pe[kGroup];             // max region end over earlier datagrams of the group
+struct GroupBuf {                    // one wave's group, in LDS (4736 B: 8 workgroups per CU)
+    uint2 ow[kGroup];                // output region start (virtual), width (0 = dropped)
     uint64_t io[kGroup];             // input payload start (absolute byte offset)
-    uint64_t salt[kGroup];           // salt (obfuscate)
     uint64_t delta[kGroup];          // real output offset - virtual offset (the run's)
     uint4 key[2 * kGroup];           // key rotated to the output's 32-byte phase, 2 halves
+    union {
+        uint64_t salt[kGroup];       // salts (obfuscate), read while boundary chunks are built
+        u128 bnd[kGroup];            // then: parked boundary chunks, XORed with the owner's key half
+    };
+    uint16_t park[kGroup];           // bits 0-2 parked (first, second, last chunk), 3-5 late, 8-15 first slot
 };
 
 // ---- BLAKE2b message words of the device block(s).  The message is
@@ -128,9 +137,9 @@ __device__ __forceinline__ void wave_key(const KeyParams& K, uint64_t salt, uint
 }
 
 // All bytes datagram k of the group contributes to the 16-byte chunk at relative a.
-template <bool OBF>
+template <bool OBF, class SaltOf>
 __device__ __forceinline__ void group_contrib(const GroupBuf& G, const uint8_t* __restrict__ in, uint32_t k,
-                                              uint32_t a, u128& r, uint32_t& cov) {
+                                              uint32_t a, u128& r, uint32_t& cov, SaltOf salt_of) {
     constexpr uint32_t SALT = OBF ? 8u : 0u;
     const uint2 owk = G.ow[k];
     const uint32_t oq = owk.x, wq = owk.y;
@@ -138,7 +147,7 @@ __device__ __forceinline__ void group_contrib(const GroupBuf& G, const uint8_t* 
     if (OBF) {   // salt bytes [oq, oq + 8)
         const uint32_t sb = max(oq, a), se = min(oq + 8u, a + 16u);
         if (sb < se) {
-            u128 S = (u128)G.salt[k];
+            u128 S = (u128)salt_of(k);
             S = oq >= a ? (S << (8 * (oq - a))) : (S >> (8 * (a - oq)));
             r |= S & bytemask(sb - a, se - a);
             cov |= ((1u << (se - sb)) - 1u) << (sb - a);
@@ -153,7 +162,11 @@ __device__ __forceinline__ void group_contrib(const GroupBuf& G, const uint8_t* 
         u128 X = 0;
         if (PL >= 16) {   // one 16-byte window inside the payload, shifted into place
             const int ws = min(max(base, 0), (int)PL - 16);
+#ifdef HY_X_NOBLOAD   // ablation builds only (timing experiments; wrong output)
+            const u128 V = (u128)(uintptr_t)(src + ws);
+#else
             const u128 V = load16u(src + ws);
+#endif
             const int d = ws - base;
             X = d >= 0 ? (V << (8 * d)) : (V >> (8 * -d));
         } else {
@@ -173,8 +186,11 @@ __device__ __forceinline__ u128 load16_nt(const uint8_t* p) {
 #ifdef HYOBFS_EMULATE
     return load16u(p);
 #else
+    // explicitly global: a generic pointer lets the compiler merge this load
+    // with the sweep's LDS read of a parked chunk into one (slow) flat load
     typedef uint32_t v4u __attribute__((ext_vector_type(4)));
-    const v4u v = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(p));
+    typedef const __attribute__((address_space(1))) v4u gv4u;
+    const v4u v = __builtin_nontemporal_load((gv4u*)(p));
     u128 r;
     __builtin_memcpy(&r, &v, 16);
     return r;
@@ -187,6 +203,26 @@ __device__ __forceinline__ uint32_t group_search(const GroupBuf& G, uint32_t a) 
 #pragma unroll
     for (uint32_t step = kGroup / 2; step; step >>= 1) qq = (G.ow[qq + step].x <= a) ? qq + step : qq;
     return qq;
+}
+
+// Where the sweep looks for a parked chunk at virtual offset a: datagram qq
+// (group_search(a), region owq) if its region reaches into the chunk, else
+// datagram qq + 1.  Returns that datagram's region in owo (width 0: none).
+__device__ __forceinline__ uint32_t park_owner(const GroupBuf& G, uint32_t a, uint32_t qq, uint2 owq, uint2& owo) {
+    if (owq.y != 0 && owq.x + owq.y > a) {
+        owo = owq;
+        return qq;
+    }
+    owo = qq + 1 < (uint32_t)kGroup ? G.ow[qq + 1] : make_uint2(0xFFFFFFFFu, 0u);
+    return qq + 1;
+}
+
+// Index of chunk c among a region's boundary candidates: 0 first chunk, 1 the
+// next one, 2 the last (when it is neither); 3: not a candidate.
+__device__ __forceinline__ uint32_t park_index(uint2 ow, uint32_t c) {
+    if (ow.y == 0) return 3u;
+    const uint32_t cs = ow.x >> 4, ce = (ow.x + ow.y - 1) >> 4;
+    return c == cs ? 0u : (c == cs + 1 && cs + 1 <= ce) ? 1u : (c == ce && ce > cs + 1) ? 2u : 3u;
 }
 
 template <bool OBF, bool PACKED, int SW>
@@ -262,11 +298,9 @@ __global__ __launch_bounds__(kGroup* kWavesPerBlock, HY_WAVE_MIN_WAVES) void sal
         const uint32_t y = __shfl_up(incm, d, 64);
         if (lane >= d) incm = max(incm, y);
     }
-    const uint32_t pe = __shfl_up(incm, 1, 64);
     const uint32_t totm = uni32(__shfl(incm, 63, 64));
     // metadata to LDS first: only salt and rel stay live through the hash
     G.ow[lane] = make_uint2(rel, W);
-    G.pe[lane] = lane ? pe : 0u;
     G.io[lane] = ioff + SKIP;
     G.delta[lane] = rb - vrun;
     if (OBF) G.salt[lane] = salt;
@@ -287,10 +321,60 @@ __global__ __launch_bounds__(kGroup* kWavesPerBlock, HY_WAVE_MIN_WAVES) void sal
     }
     hy_wave_sync();
 
-    // ---- 3. sweep: virtual chunks inside one payload.  (Finishing the
-    // boundary chunks here instead, so that whole 128-byte lines leave in one
-    // wave instruction, measured slower: the divergent byte merging costs
-    // more than the partial-line write-backs it saves.)
+    // ---- 3. boundary chunks datagram `lane` owns (the first datagram touching a
+    // chunk owns it: exclusive max-scan of region ends) that are not inside one
+    // payload.  A complete one that the sweep's lookup (park_owner/park_index)
+    // maps back to this lane is parked; the rest are stored late (step 5).
+    // (Merging these bytes inside the sweep instead measured slower: the
+    // divergent byte merging cost more than the partial lines it saved.)
+    {
+        uint32_t parkm = 0, want = 0;
+        u128 bv[3] = {0, 0, 0};
+        const uint32_t pe0 = __shfl_up(incm, 1, 64);   // max region end over earlier datagrams
+        const uint32_t pe = lane ? pe0 : 0u;
+#ifndef HY_X_NOBOUND
+        if (W) {
+            const uint32_t st = rel, en = rel + W;
+            const uint32_t cs = st >> 4, ce = (en - 1) >> 4;
+            const uint32_t cand[3] = {cs, cs + 1, ce};
+            const bool use[3] = {pe <= (cs << 4), cs + 1 <= ce, ce > cs + 1};
+#pragma unroll
+            for (int t = 0; t < 3; ++t) {
+                const uint32_t a = cand[t] << 4;
+                if (!use[t] || (st + SALT <= a && a + 16 <= en)) continue;   // inside the payload: swept
+                want |= 1u << t;
+                u128 rr = 0;
+                uint32_t cov = 0;
+                for (uint32_t k = lane; k < cnt && G.ow[k].x < a + 16; ++k)
+                    group_contrib<OBF>(G, in, k, a, rr, cov, [&](uint32_t kk) { return G.salt[kk]; });
+                const uint32_t qq = group_search(G, a);
+                uint2 owo;
+                const uint32_t o = park_owner(G, a, qq, G.ow[qq], owo);
+                if (cov == 0xFFFFu && o == (uint32_t)lane && park_index(owo, cand[t]) == (uint32_t)t) {
+                    const uint4 kk = G.key[2 * lane + ((a >> 4) & 1)];
+                    u128 k128;
+                    __builtin_memcpy(&k128, &kk, 16);
+                    bv[t] = rr ^ k128;   // the sweep XORs the owner's key half back in
+                    parkm |= 1u << t;
+                }
+            }
+        }
+#else
+        (void)pe;
+#endif
+        const uint32_t np = (uint32_t)__builtin_popcount(parkm);
+        const uint32_t base = (uint32_t)wave_incl_scan(np, lane) - np;
+        if (base + np > (uint32_t)kGroup) parkm = 0;   // out of slots: store late
+        hy_wave_sync();   // every lane has read the salts the slots overwrite
+        uint32_t sl = base;
+#pragma unroll
+        for (int t = 0; t < 3; ++t)
+            if ((parkm >> t) & 1u) G.bnd[sl++] = bv[t];
+        G.park[lane] = (uint16_t)(parkm | ((want & ~parkm) << 3) | (base << 8));
+    }
+    hy_wave_sync();
+
+    // ---- 4. sweep: virtual chunks inside one payload, and parked chunks
     const uint32_t nchunks = (totm + 15u) >> 4;
     struct Sweep {   // one iteration's loads in flight
         u128 v[U];
@@ -307,7 +391,24 @@ __global__ __launch_bounds__(kGroup* kWavesPerBlock, HY_WAVE_MIN_WAVES) void sal
             const uint2 owq = G.ow[qq];
             R.fast[u] = (c < nchunks) && owq.y != 0 && owq.x + SALT <= a && a + 16 <= owq.x + owq.y;
             R.v[u] = 0;
-            if (R.fast[u]) R.v[u] = load16_nt(in + G.io[qq] + (a - owq.x - SALT));
+            if (R.fast[u]) {
+                R.v[u] = load16_nt(in + G.io[qq] + (a - owq.x - SALT));
+            }
+#ifndef HY_X_NOPARK
+            else if (c < nchunks) {   // parked boundary chunk?
+                uint2 owo;
+                const uint32_t o = park_owner(G, a, qq, owq, owo);
+                const uint32_t t = park_index(owo, c);
+                if (t < 3) {
+                    const uint32_t pk = G.park[o];
+                    if ((pk >> t) & 1u) {
+                        R.fast[u] = true;
+                        R.q[u] = o;
+                        R.v[u] = G.bnd[(pk >> 8) + (uint32_t)__builtin_popcount(pk & ((1u << t) - 1u))];
+                    }
+                }
+            }
+#endif
         }
     };
     auto retire = [&](uint32_t c0, const Sweep& R) {
@@ -341,27 +442,25 @@ __global__ __launch_bounds__(kGroup* kWavesPerBlock, HY_WAVE_MIN_WAVES) void sal
     }
 #endif
 
-    // ---- 4. boundary: chunks datagram `lane` owns that are not inside one payload
-    const uint2 own = G.ow[lane];
-#ifdef HY_X_NOBOUND   // ablation builds only (timing experiments; wrong output)
-    if (false) {
-#else
-    if (own.y) {
-#endif
+    // ---- 5. late boundary chunks (not parked): byte-masked stores.  The salt
+    // slots now hold parked chunks, so salts come from the batch.
+    const uint32_t late = (uint32_t)(G.park[lane] >> 3) & 7u;
+    if (late) {
+        const uint2 own = G.ow[lane];
         const uint32_t st = own.x, en = own.x + own.y;
         const uint32_t cs = st >> 4, ce = (en - 1) >> 4;
-        const bool own_cs = G.pe[lane] <= (cs << 4);
         const uint32_t cand[3] = {cs, cs + 1, ce};
-        const bool use[3] = {own_cs, cs + 1 <= ce, ce > cs + 1};
         uint8_t* outb = B.out + G.delta[lane];   // a chunk's contributors share its run
+        auto salt_of = [&](uint32_t k) {   // datagram index of lane k: its run, then its place in the run
+            return B.salts[((((uint64_t)(k >> rl)) * Wt + w) << rl) + (k & (RUN - 1))];
+        };
 #pragma unroll
         for (int t = 0; t < 3; ++t) {
-            if (!use[t]) continue;
+            if (!((late >> t) & 1u)) continue;
             const uint32_t a = cand[t] << 4;
-            if (st + SALT <= a && a + 16 <= en) continue;   // inside the payload: swept
             u128 rr = 0;
             uint32_t cov = 0;
-            for (uint32_t k = lane; k < cnt && G.ow[k].x < a + 16; ++k) group_contrib<OBF>(G, in, k, a, rr, cov);
+            for (uint32_t k = lane; k < cnt && G.ow[k].x < a + 16; ++k) group_contrib<OBF>(G, in, k, a, rr, cov, salt_of);
             if (cov) store_masked(outb + a, rr, cov);
         }
     }

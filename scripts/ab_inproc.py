@@ -13,7 +13,7 @@ import torch  # noqa: E402
 from hysteria_amd import _lib  # noqa: E402
 
 libs = sys.argv[1:] or ["hysteria_amd/libhyobfs.so"]
-P, L = 1 << 20, 1200
+P, L = 1 << 20, int(os.environ.get("AB_LEN", "1200"))
 workload = os.environ.get("AB_WORKLOAD", "uniform")
 dev = torch.device("cuda:0")
 main = _lib.load(os.path.abspath(libs[0]))
