@@ -11,8 +11,10 @@ from .salamander import (  # noqa: F401
     UDP_BUFFER_SIZE,
     PSKTooShortError,
     SalamanderObfuscator,
+    deobfuscate_batch_sharded,
     device_count,
     new_salamander_obfuscator,
+    obfuscate_batch_sharded,
     synth_bimodal_lengths,
     synth_stream,
     synth_u64,
@@ -23,4 +25,5 @@ __all__ = [
     "SM_KEY_LEN", "SM_PSK_MIN_LEN", "SM_SALT_LEN", "UDP_BUFFER_SIZE", "PSKTooShortError",
     "SalamanderObfuscator", "device_count", "new_salamander_obfuscator", "synth_bimodal_lengths",
     "synth_stream", "synth_u64", "workspace_size", "SalamanderPacketConn", "wrap_packet_conn_salamander",
+    "obfuscate_batch_sharded", "deobfuscate_batch_sharded",
 ]

@@ -103,6 +103,9 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         "hyobfs_batch_workspace_size": (u64, [u64]),
         "hyobfs_salamander_obfuscate_batch": (i32, [pctx, ctypes.POINTER(HyobfsBatch), vp]),
         "hyobfs_salamander_deobfuscate_batch": (i32, [pctx, ctypes.POINTER(HyobfsBatch), vp]),
+        "hyobfs_salamander_obfuscate_batch_sharded": (i32, [vp, ctypes.POINTER(HyobfsBatch), i32]),
+        "hyobfs_salamander_deobfuscate_batch_sharded": (i32, [vp, ctypes.POINTER(HyobfsBatch), i32]),
+        "hyobfs_shard_bounds": (i32, [vp, u64, i32, vp]),
         "hyobfs_salamander_obfuscate_host": (i32, [pctx, ctypes.POINTER(HyobfsBatch), u64]),
         "hyobfs_salamander_deobfuscate_host": (i32, [pctx, ctypes.POINTER(HyobfsBatch), u64]),
         "hyobfs_host_alloc": (vp, [sz]),

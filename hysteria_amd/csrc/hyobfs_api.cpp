@@ -307,6 +307,27 @@ int run_batch(hyobfs_salamander* c, const hyobfs_batch* b, void* stream, bool ob
 }
 
 
+// One batch per shard, each on its own context's stream (and device): launch all, then wait for all.
+int run_sharded(hyobfs_salamander* const* ctxs, const hyobfs_batch* batches, int nshards, bool obf) {
+    if (nshards < 0 || (nshards && (!ctxs || !batches))) return HYOBFS_ERR_INVALID;
+    for (int i = 0; i < nshards; ++i) {
+        if (!ctxs[i]) return HYOBFS_ERR_INVALID;
+        for (int j = 0; j < i; ++j)
+            if (ctxs[j] == ctxs[i]) return HYOBFS_ERR_INVALID;   // one context (stream) per shard
+    }
+    int rc = HYOBFS_OK;
+    int launched = 0;
+    for (; launched < nshards; ++launched) {
+        rc = run_batch(ctxs[launched], &batches[launched], ctxs[launched]->stream, obf);
+        if (rc != HYOBFS_OK) break;
+    }
+    for (int i = 0; i < launched; ++i) {   // drain what was launched, even after a failure
+        DeviceGuard g(ctxs[i]->device);
+        if ((!g.ok || hipStreamSynchronize(ctxs[i]->stream) != hipSuccess) && rc == HYOBFS_OK) rc = HYOBFS_ERR_HIP;
+    }
+    return rc;
+}
+
 // Grow a device buffer (caller holds the pipeline lock; the slot's stream is idle).
 template <class T>
 int grow(T*& p, uint64_t& cap, uint64_t need_bytes) {
@@ -562,6 +583,36 @@ int hyobfs_salamander_obfuscate_batch(hyobfs_salamander* c, const hyobfs_batch* 
 
 int hyobfs_salamander_deobfuscate_batch(hyobfs_salamander* c, const hyobfs_batch* b, void* stream) {
     return run_batch(c, b, stream, false);
+}
+
+int hyobfs_salamander_obfuscate_batch_sharded(hyobfs_salamander* const* ctxs, const hyobfs_batch* batches,
+                                              int nshards) {
+    return run_sharded(ctxs, batches, nshards, true);
+}
+
+int hyobfs_salamander_deobfuscate_batch_sharded(hyobfs_salamander* const* ctxs, const hyobfs_batch* batches,
+                                                int nshards) {
+    return run_sharded(ctxs, batches, nshards, false);
+}
+
+int hyobfs_shard_bounds(const uint32_t* in_len, uint64_t n, int nshards, uint64_t* bounds) {
+    if (nshards <= 0 || !bounds) return HYOBFS_ERR_INVALID;
+    bounds[0] = 0;
+    if (!in_len) {   // equal counts, the remainder spread over the first shards
+        for (int i = 1; i <= nshards; ++i) bounds[i] = n / nshards * i + std::min<uint64_t>(n % nshards, i);
+        return HYOBFS_OK;
+    }
+    uint64_t total = 0;
+    for (uint64_t k = 0; k < n; ++k) total += (uint64_t)in_len[k] + 8;
+    // shard i starts at the first datagram whose preceding weight reaches total * i / nshards
+    uint64_t acc = 0, k = 0;
+    for (int i = 1; i < nshards; ++i) {
+        const unsigned __int128 target = (unsigned __int128)total * (unsigned)i / (unsigned)nshards;
+        while (k < n && acc < target) acc += (uint64_t)in_len[k++] + 8;
+        bounds[i] = k;
+    }
+    bounds[nshards] = n;
+    return HYOBFS_OK;
 }
 
 int hyobfs_salamander_obfuscate_host(hyobfs_salamander* c, const hyobfs_batch* b, uint64_t chunk) {

@@ -86,6 +86,19 @@ def _stream(stream, *tensors):
     return None
 
 
+def _make_batch(*, inp, n, in_off=None, in_stride=0, in_len=None, len_uniform=0, salts=None, out,
+                out_cap=None, out_stride=0, pkt_cap=0, out_off=None, out_len=None, out_total=None,
+                workspace=None, workspace_bytes=0) -> HyobfsBatch:
+    """struct hyobfs_batch from device tensors (layout rules: include/hyobfs.h)."""
+    if out_cap is None:
+        out_cap = out.numel() * out.element_size() if hasattr(out, "numel") else 0
+    return HyobfsBatch(n=n, in_=_ptr(inp), in_off=_ptr(in_off), in_stride=in_stride,
+                       in_len=_ptr(in_len), len_uniform=len_uniform, pkt_cap=pkt_cap,
+                       salts=_ptr(salts), out=_ptr(out), out_cap=out_cap, out_stride=out_stride,
+                       out_off=_ptr(out_off), out_len=_ptr(out_len), out_total=_ptr(out_total),
+                       workspace=_ptr(workspace), workspace_bytes=workspace_bytes)
+
+
 class SalamanderObfuscator:
     """A Salamander obfuscator bound to one MI355X (HIP device ``device``)."""
 
@@ -172,17 +185,9 @@ class SalamanderObfuscator:
         return self._lib.hyobfs_salamander_deobfuscate(self._h, ip, il, op, ol)
 
     # ------------------------------------------------------------------ batch
-    def _batch(self, obf, *, inp, n, in_off=None, in_stride=0, in_len=None, len_uniform=0,
-               salts=None, out, out_cap=None, out_stride=0, pkt_cap=0, out_off=None,
-               out_len=None, out_total=None, workspace=None, workspace_bytes=0, stream=None):
-        if out_cap is None:
-            out_cap = out.numel() * out.element_size() if hasattr(out, "numel") else 0
-        b = HyobfsBatch(n=n, in_=_ptr(inp), in_off=_ptr(in_off), in_stride=in_stride,
-                        in_len=_ptr(in_len), len_uniform=len_uniform, pkt_cap=pkt_cap,
-                        salts=_ptr(salts), out=_ptr(out), out_cap=out_cap, out_stride=out_stride,
-                        out_off=_ptr(out_off), out_len=_ptr(out_len), out_total=_ptr(out_total),
-                        workspace=_ptr(workspace), workspace_bytes=workspace_bytes)
-        s = _stream(stream, inp, out)
+    def _batch(self, obf, *, stream=None, **kw):
+        b = _make_batch(**kw)
+        s = _stream(stream, kw["inp"], kw["out"])
         f = self._lib.hyobfs_salamander_obfuscate_batch if obf else self._lib.hyobfs_salamander_deobfuscate_batch
         check(f(self._h, ctypes.byref(b), s), "obfuscate_batch" if obf else "deobfuscate_batch")
 
@@ -224,6 +229,26 @@ class SalamanderObfuscator:
 def new_salamander_obfuscator(psk: bytes, device: int = 0) -> SalamanderObfuscator:
     """newSalamanderObfuscator (salamander.go:34-46)."""
     return SalamanderObfuscator(psk, device)
+
+
+def _sharded(obf, obfuscators, shards) -> None:
+    if len(obfuscators) != len(shards):
+        raise ValueError("one obfuscator (context) per shard")
+    lib = _lib.load()
+    arr = (HyobfsBatch * len(shards))(*[_make_batch(**kw) for kw in shards])
+    ctxs = (ctypes.c_void_p * len(shards))(*[o._h for o in obfuscators])
+    f = lib.hyobfs_salamander_obfuscate_batch_sharded if obf else lib.hyobfs_salamander_deobfuscate_batch_sharded
+    check(f(ctxs, arr, len(shards)), "obfuscate_batch_sharded" if obf else "deobfuscate_batch_sharded")
+
+
+def obfuscate_batch_sharded(obfuscators, shards) -> None:
+    """Shard i (keyword dict of obfuscate_batch's arguments, tensors on the device of
+    obfuscators[i]) runs on obfuscators[i]'s stream; returns when every shard is done."""
+    _sharded(True, obfuscators, shards)
+
+
+def deobfuscate_batch_sharded(obfuscators, shards) -> None:
+    _sharded(False, obfuscators, shards)
 
 
 def device_count() -> int:

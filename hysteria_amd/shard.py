@@ -19,10 +19,12 @@ def even_split(n: int, world: int, rank: int) -> tuple[int, int]:
 
 
 def byte_balanced_split(lengths: np.ndarray, world: int, rank: int) -> tuple[int, int]:
-    """(first, count) splitting a ragged batch so each rank gets ~equal payload bytes.
+    """(first, count) splitting a ragged batch so each rank gets ~equal traffic.
 
-    Boundary k sits at the first datagram whose exclusive byte prefix reaches
-    k/world of the total ("split by cumulative bytes").
+    Datagram k weighs lengths[k] + 8 (its bytes plus the salt), and boundary j
+    sits at the first datagram whose exclusive weight prefix reaches j/world of
+    the total ("split by cumulative bytes").  Same rule as the C ABI's
+    hyobfs_shard_bounds (include/hyobfs.h).
     """
     if world < 1 or not 0 <= rank < world:
         raise ValueError("bad world/rank")
@@ -31,7 +33,7 @@ def byte_balanced_split(lengths: np.ndarray, world: int, rank: int) -> tuple[int
     if n == 0:
         return 0, 0
     excl = np.zeros(n + 1, dtype=np.uint64)
-    np.cumsum(lengths, out=excl[1:])
+    np.cumsum(lengths + np.uint64(8), out=excl[1:])
     total = int(excl[-1])
 
     def cut(k: int) -> int:
@@ -43,6 +45,23 @@ def byte_balanced_split(lengths: np.ndarray, world: int, rank: int) -> tuple[int
 
     a, b = cut(rank), cut(rank + 1)
     return a, b - a
+
+
+def shard_bounds(lengths, n: int, world: int) -> list[int]:
+    """bounds[0..world] of every rank's range, from the C ABI (hyobfs_shard_bounds).
+
+    lengths=None: a uniform batch (split by count).  Host-only call, no device."""
+    import ctypes
+
+    from . import _lib
+    out = (ctypes.c_uint64 * (world + 1))()
+    if lengths is None:
+        ptr = None
+    else:
+        arr = np.ascontiguousarray(lengths, dtype=np.uint32)
+        ptr = arr.ctypes.data
+    _lib.check(_lib.load().hyobfs_shard_bounds(ptr, n, world, out), "shard_bounds")
+    return list(out)
 
 
 def weak_shard(per_rank: int, rank: int) -> tuple[int, int]:

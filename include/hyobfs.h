@@ -177,6 +177,30 @@ int hyobfs_salamander_obfuscate_batch(hyobfs_salamander* ctx, const hyobfs_batch
 int hyobfs_salamander_deobfuscate_batch(hyobfs_salamander* ctx, const hyobfs_batch* b,
                                         void* stream);
 
+/* ---------------------------------------------------- multi-GPU shards */
+/*
+ * The path shards by datagram index with no exchange step: every datagram
+ * depends only on (PSK, salt, payload) (salamander.go:59-86), so shard i is
+ * an ordinary batch on the device of ctxs[i], with buffers on that device.
+ * The sharded calls launch every shard on its context's stream, then wait
+ * for all of them; the return value is the first failing shard's status
+ * (HYOBFS_OK when all succeed).  Contexts must be distinct (one per shard);
+ * two shards may share a device.  No collective and no peer traffic.
+ */
+int hyobfs_salamander_obfuscate_batch_sharded(hyobfs_salamander* const* ctxs,
+                                              const hyobfs_batch* batches, int nshards);
+int hyobfs_salamander_deobfuscate_batch_sharded(hyobfs_salamander* const* ctxs,
+                                                const hyobfs_batch* batches, int nshards);
+/*
+ * Shard planning (host only, no device call): split datagrams [0, n) into
+ * nshards contiguous index ranges [bounds[i], bounds[i+1]) of equal traffic,
+ * weighting datagram k by in_len[k] + 8 (its wire or payload bytes; a
+ * ragged batch is split by cumulative bytes, a uniform one by count).
+ * in_len == NULL means every datagram has the same length.  bounds has
+ * nshards + 1 entries, bounds[0] = 0 and bounds[nshards] = n.
+ */
+int hyobfs_shard_bounds(const uint32_t* in_len, uint64_t n, int nshards, uint64_t* bounds);
+
 /* ------------------------------------------------- host-resident batches */
 /*
  * The path starts and ends in host memory (UDP socket buffers).  These calls

@@ -423,3 +423,70 @@ def test_packet_conn_loopback(gpu):
     batched recvmmsg/sendmmsg paths, wire bytes against the oracle."""
     from conn_cases import run_conn_scenarios
     run_conn_scenarios(device=0, batch=1024, n_batch=400)
+
+
+# ------------------------------------------------------------- sharded batches
+@pytest.mark.parametrize("nshards", [1, 2, 3])
+def test_sharded_batch_matches_single_batch(gpu, coracle, nshards):
+    """hyobfs_salamander_*_batch_sharded: shards planned by hyobfs_shard_bounds (equal
+    traffic), one context each (all on device 0 here), packed outputs per shard.  The
+    shards' outputs back to back are the single batch's packed output."""
+    import torch
+    import hysteria_amd
+    from hysteria_amd.shard import shard_bounds
+    n = 20_000
+    lens, in_off, inp, salts, total_in = _bimodal(gpu, n)
+    h_lens = _host(lens).view(np.uint32)
+    bounds = shard_bounds(h_lens, n, nshards)
+    exp, eoff, elen, _ = coracle.batch(True, PSK, n, _host(inp), in_off=_host(in_off).view(np.uint64),
+                                       in_len=h_lens, salts=coracle.salts(2, 0, n), out_cap=total_in + 8 * n)
+    ctxs = [hysteria_amd.SalamanderObfuscator(PSK, 0) for _ in range(nshards)]
+    try:
+        shards, outs, back_shards, backs = [], [], [], []
+        for i in range(nshards):
+            a, b = bounds[i], bounds[i + 1]
+            cap = int(h_lens[a:b].astype(np.uint64).sum()) + 8 * (b - a)
+            out = torch.empty(max(cap, 16), dtype=torch.uint8, device=gpu)
+            olen = torch.empty(max(b - a, 1), dtype=torch.int32, device=gpu)
+            ooff = torch.empty(max(b - a, 1), dtype=torch.int64, device=gpu)
+            ws = torch.empty(hysteria_amd.workspace_size(b - a), dtype=torch.uint8, device=gpu)
+            outs.append((out, ooff, olen, cap, a, b))
+            shards.append(dict(inp=inp, n=b - a, in_off=in_off[a:], in_len=lens[a:], salts=salts[a:], out=out,
+                               out_cap=cap, out_off=ooff, out_len=olen, workspace=ws, workspace_bytes=ws.numel()))
+        hysteria_amd.obfuscate_batch_sharded(ctxs, shards)
+        got = np.concatenate([_host(o)[:cap] for o, _, _, cap, _, _ in outs])
+        assert np.array_equal(got, exp[:total_in + 8 * n])
+        base = 0
+        for o, ooff, olen, cap, a, b in outs:
+            if b > a:
+                assert np.array_equal(_host(ooff)[:b - a].view(np.uint64) + np.uint64(base), eoff[a:b])
+                assert np.array_equal(_host(olen)[:b - a].view(np.uint32), elen[a:b])
+            base += cap
+        # and back, sharded the same way
+        for o, ooff, olen, cap, a, b in outs:
+            plen = cap - 8 * (b - a)
+            back = torch.empty(max(plen, 16), dtype=torch.uint8, device=gpu)
+            backs.append((back, plen))
+            back_shards.append(dict(inp=o, n=b - a, in_off=ooff, in_len=olen, out=back, out_cap=plen))
+        hysteria_amd.deobfuscate_batch_sharded(ctxs, back_shards)
+        plain = np.concatenate([_host(bk)[:plen] for bk, plen in backs])
+        assert np.array_equal(plain, _host(inp)[:total_in])
+    finally:
+        for c in ctxs:
+            c.close()
+
+
+def test_sharded_batch_argument_errors(gpu):
+    import ctypes
+    import hysteria_amd
+    from hysteria_amd import _lib
+    lib = _lib.load()
+    o = hysteria_amd.SalamanderObfuscator(PSK, 0)
+    try:
+        arr = (_lib.HyobfsBatch * 2)()
+        dup = (ctypes.c_void_p * 2)(o._h, o._h)
+        assert lib.hyobfs_salamander_obfuscate_batch_sharded(dup, arr, 2) == _lib.HYOBFS_ERR_INVALID
+        assert lib.hyobfs_salamander_obfuscate_batch_sharded(None, None, 0) == _lib.HYOBFS_OK
+        assert lib.hyobfs_salamander_deobfuscate_batch_sharded(None, arr, 1) == _lib.HYOBFS_ERR_INVALID
+    finally:
+        o.close()

@@ -33,9 +33,9 @@ def test_byte_balanced_split_partitions_and_balances():
             first, cnt = byte_balanced_split(lens, world, r)
             assert first == seen
             seen += cnt
-            shares.append(int(lens[first:first + cnt].sum()))
+            shares.append(int(lens[first:first + cnt].sum()) + 8 * cnt)   # weight len + 8
         assert seen == lens.size
-        assert max(shares) - min(shares) <= 2 * 1350
+        assert max(shares) - min(shares) <= 2 * (1350 + 8)
 
 
 def test_weak_shard():
@@ -89,3 +89,15 @@ def test_gloo_two_ranks_shards_concatenate_to_whole(tmp_path):
     whole, _, _, _ = co.batch(True, PSK, n, inp, in_off=in_off, in_len=lens, salts=co.salts(2, 0, n),
                               out_cap=int(lens.sum()) + 8 * n)
     assert (tmp_path / "joined.bin").read_bytes() == whole.tobytes()
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+def test_c_abi_shard_bounds_match_host_mirror(world):
+    """hyobfs_shard_bounds (C ABI, host-only) and hysteria_amd.shard give the same ranges."""
+    from hysteria_amd.shard import shard_bounds
+    lens = ref.bimodal_lengths(3, 0, 20_000)
+    b = shard_bounds(lens, lens.size, world)
+    assert b == [byte_balanced_split(lens, world, r)[0] for r in range(world)] + [lens.size]
+    for n in (0, 1, 7, 1 << 20):
+        u = shard_bounds(None, n, world)
+        assert u == [even_split(n, world, r)[0] for r in range(world)] + [n]
