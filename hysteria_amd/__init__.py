@@ -3,7 +3,9 @@
 The product is ``libhyobfs.so`` (gfx950 HIP kernels behind the C ABI of
 ``include/hyobfs.h``); this package is its Python host binding.
 """
+from . import gecko  # noqa: F401
 from .conn import SalamanderPacketConn, wrap_packet_conn_salamander  # noqa: F401
+from .gecko import GeckoOptions, GeckoPacketConn, wrap_packet_conn_gecko  # noqa: F401
 from .salamander import (  # noqa: F401
     SM_KEY_LEN,
     SM_PSK_MIN_LEN,
@@ -25,5 +27,6 @@ __all__ = [
     "SM_KEY_LEN", "SM_PSK_MIN_LEN", "SM_SALT_LEN", "UDP_BUFFER_SIZE", "PSKTooShortError",
     "SalamanderObfuscator", "device_count", "new_salamander_obfuscator", "synth_bimodal_lengths",
     "synth_stream", "synth_u64", "workspace_size", "SalamanderPacketConn", "wrap_packet_conn_salamander",
-    "obfuscate_batch_sharded", "deobfuscate_batch_sharded",
+    "obfuscate_batch_sharded", "deobfuscate_batch_sharded", "gecko", "GeckoOptions", "GeckoPacketConn",
+    "wrap_packet_conn_gecko",
 ]

@@ -615,6 +615,29 @@ int hyobfs_shard_bounds(const uint32_t* in_len, uint64_t n, int nshards, uint64_
     return HYOBFS_OK;
 }
 
+uint64_t hyobfs_gecko_workspace_size(uint64_t n) { return 32 * n; }
+
+int hyobfs_gecko_encode_batch(hyobfs_salamander* c, const hyobfs_gecko_batch* b, void* stream) {
+    if (!c || !b) return HYOBFS_ERR_INVALID;
+    if (b->n == 0) return HYOBFS_OK;
+    if (!b->msg || !b->frames || !b->salts || !b->out || !b->out_off || !b->workspace ||
+        b->workspace_bytes < hyobfs_gecko_workspace_size(b->n))
+        return HYOBFS_ERR_INVALID;
+    DeviceGuard g(c->device);
+    if (!g.ok) return HYOBFS_ERR_HIP;
+    return hyobfs::launch_gecko_encode(c->kp, *b, static_cast<hipStream_t>(stream)) == hipSuccess ? HYOBFS_OK
+                                                                                                : HYOBFS_ERR_HIP;
+}
+
+int hyobfs_gecko_parse_batch(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint64_t n,
+                             hyobfs_gecko_parsed* out, void* stream) {
+    if (n == 0) return HYOBFS_OK;
+    if (!in || !in_off || !in_len || !out) return HYOBFS_ERR_INVALID;
+    return hyobfs::launch_gecko_parse(in, in_off, in_len, n, out, static_cast<hipStream_t>(stream)) == hipSuccess
+               ? HYOBFS_OK
+               : HYOBFS_ERR_HIP;
+}
+
 int hyobfs_salamander_obfuscate_host(hyobfs_salamander* c, const hyobfs_batch* b, uint64_t chunk) {
     return run_host(c, b, chunk, true);
 }

@@ -10,6 +10,8 @@
 #include <cstdlib>
 #include <cstring>
 
+#include "../../include/hyobfs_gecko.h"
+
 namespace hyobfs {
 
 // Orders one wave's LDS writes before its later LDS reads by other lanes of the
@@ -75,6 +77,9 @@ hipError_t launch_salamander(bool obfuscate, const BatchParams& b, const KeyPara
                              hipStream_t s);
 hipError_t launch_keys(const KeyParams& k, const uint64_t* salts, uint8_t* keys, uint64_t n,
                        hipStream_t s);
+hipError_t launch_gecko_encode(const KeyParams& k, const hyobfs_gecko_batch& b, hipStream_t s);
+hipError_t launch_gecko_parse(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint64_t n,
+                              hyobfs_gecko_parsed* out, hipStream_t s);
 hipError_t launch_synth_stream(uint8_t* dst, uint64_t nbytes, uint64_t seed, uint64_t start,
                                hipStream_t s);
 hipError_t launch_synth_u64(uint64_t* dst, uint64_t n, uint64_t seed, uint64_t first,

@@ -148,6 +148,51 @@ def case_host(n, L, chunk, obf):
         assert out[i * out_stride:i * out_stride + len(exp)].tobytes() == exp, i
 
 
+def case_gecko(n_msgs, seed):
+    """Gecko frames: one device encode pass vs oracle/gecko_ref, then deobfuscate + parse."""
+    from hysteria_amd import gecko
+    from oracle import gecko_ref as gref
+    psk = b"average_password"
+    rng = np.random.default_rng(seed)
+    lens = rng.integers(1, 1400, n_msgs)
+    lens[:3] = [1, 5, 2000][:min(3, n_msgs)]
+    msg = rng.integers(0, 256, int(lens.sum()) + 16, dtype=np.uint8)
+    fr, off, total = gecko.plan_fragments(lens, 400, 900, first_msg_id=seed)
+    nf = len(fr)
+    salts = ref.splitmix64_array(5, 0, nf)
+    out = np.full(total + 64, 0xA5, np.uint8)
+    ws = np.zeros(gecko.workspace_size(nf), np.uint8)
+    o = SalamanderObfuscator(psk, 0)
+    p = lambda a: a.ctypes.data  # noqa: E731
+    gecko.encode_batch(o, msg=p(msg), frames=p(fr), salts=p(salts), pad_seed=99, out=p(out), out_off=p(off),
+                       workspace=p(ws), n=nf, stream=0)
+    exp = gref.encode_wire(psk, msg.tobytes(), fr.tolist(), salts, 99)
+    assert out[total:].tobytes() == b"\xa5" * 64
+    for i in range(nf):
+        assert out[int(off[i]):int(off[i]) + len(exp[i])].tobytes() == exp[i], i
+    # back: Salamander deobfuscate batch, then the Gecko parse kernel
+    wl = np.array([len(e) for e in exp], np.uint32)
+    plain = np.zeros(total, np.uint8)
+    poff = np.zeros(nf, np.uint64)
+    plen = np.zeros(nf, np.uint32)
+    o.deobfuscate_batch(p(out), nf, in_off=p(off), in_len=p(wl), out=p(plain), out_cap=total, out_off=p(poff),
+                        out_len=p(plen), stream=0)
+    parsed = np.zeros(nf + 1, gecko.PARSED_DTYPE)
+    garbage = np.frombuffer(bytes([0x80, 1, 0x44, 0, 0]), np.uint8).copy()
+    gecko.parse_batch(p(plain), p(poff), p(plen), nf, p(parsed), stream=0)
+    o.close()
+    for i in range(nf):
+        d = plain[int(poff[i]):int(poff[i]) + int(plen[i])].tobytes()
+        kind, h, payload = gref.parse(d)
+        assert kind == gref.FRAGMENT and int(parsed[i]["status"]) == gecko.FRAGMENT, i
+        assert int(parsed[i]["msg_id"]) == h.msg_id and int(parsed[i]["pad_len"]) == h.pad_len
+        assert int(parsed[i]["idx_total"]) == (h.chunk_idx << 4 | h.total_chunks)
+        po, pl = int(parsed[i]["payload_off"]), int(parsed[i]["payload_len"])
+        assert d[po:po + pl] == payload
+    gecko.parse_batch(p(garbage), p(np.zeros(1, np.uint64)), p(np.array([5], np.uint32)), 1, p(parsed), stream=0)
+    assert int(parsed[0]["status"]) == gecko.ERR_INVALID
+
+
 if __name__ == "__main__":
     lib = _lib.load()
     which = sys.argv[1]
@@ -166,5 +211,7 @@ if __name__ == "__main__":
         case_slotted_far(args[0], args[1], args[2], bool(args[3]))
     elif which == "ragged":
         case_ragged(args[0], args[1], args[2], bool(args[3]), ["packed", "slotted"][args[4]])
+    elif which == "gecko":
+        case_gecko(args[0], args[1])
     print("ok", which, args)
 

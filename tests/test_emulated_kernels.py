@@ -47,6 +47,7 @@ CASES = [
     ("conn", "64 120", "2"),             # UDP loopback through the conn wrapper (conn.go)
     ("far", "200 300 15 1", "8"),        # workgroup bases beyond 2^31
     ("far", "200 300 15 0", "8"),
+    ("gecko", "40 7", "2"),              # Gecko frame encode + parse kernels (gecko.hip)
 ]
 
 

@@ -1,0 +1,178 @@
+"""Gecko on the GPU: the one-pass frame encode kernel and the parse kernel
+(include/hyobfs_gecko.h) against oracle/gecko_ref.py, reassembly of the parsed
+fragments through the host GeckoPacketConn, and the full Gecko-over-Salamander
+packet conn on a loopback UDP socket (gecko.go:34-55, gecko_test.go round trips)."""
+import random
+import socket
+
+import numpy as np
+import pytest
+
+from oracle import gecko_ref as gref
+from oracle import salamander_ref as sref
+
+pytestmark = pytest.mark.gpu
+PSK = b"average_password"
+
+
+def _dev(a, gpu):
+    import torch
+    return torch.from_numpy(np.ascontiguousarray(a).view(np.uint8)).to(gpu)
+
+
+def _messages(n, seed):
+    rng = np.random.default_rng(seed)
+    lens = rng.integers(1, 1400, n)
+    lens[:4] = [1, 5, 27, 2000][:min(4, n)]
+    msg = rng.integers(0, 256, int(lens.sum()) + 16, dtype=np.uint8)
+    return lens, msg
+
+
+@pytest.mark.parametrize("n_msgs,lo,hi", [(1, 512, 1200), (300, 512, 1200), (500, 400, 900), (64, 2048, 2048)])
+def test_encode_batch_vs_oracle(gpu, n_msgs, lo, hi):
+    import torch
+    import hysteria_amd
+    from hysteria_amd import gecko
+    lens, msg = _messages(n_msgs, n_msgs + lo)
+    fr, off, total = gecko.plan_fragments(lens, lo, hi, first_msg_id=3)
+    nf = len(fr)
+    salts = sref.splitmix64_array(5, 0, nf)
+    o = hysteria_amd.SalamanderObfuscator(PSK, 0)
+    try:
+        out = torch.full((total + 64,), 0xA5, dtype=torch.uint8, device=gpu)
+        ws = torch.empty(gecko.workspace_size(nf), dtype=torch.uint8, device=gpu)
+        gecko.encode_batch(o, msg=_dev(msg, gpu), frames=_dev(fr, gpu), salts=_dev(salts, gpu), pad_seed=1234,
+                           out=out, out_off=_dev(off, gpu), workspace=ws, n=nf)
+        got = out.cpu().numpy()
+    finally:
+        o.close()
+    exp = gref.encode_wire(PSK, msg.tobytes(), fr.tolist(), salts, 1234)
+    assert got[total:].tobytes() == b"\xa5" * 64
+    for i in range(nf):
+        assert got[int(off[i]):int(off[i]) + len(exp[i])].tobytes() == exp[i], i
+        w = len(exp[i])
+        assert w <= hi or int(fr[i]["pad_len"]) == 0
+        assert w >= lo or 13 + int(fr[i]["chunk_len"]) > hi
+
+
+def test_encode_batch_skips_impossible_frames(gpu):
+    import torch
+    import hysteria_amd
+    from hysteria_amd import gecko
+    msg = np.arange(64, dtype=np.uint8)
+    fr = np.array([(0, 10, 0, 1, 0x02), (0, 10, 0, 1, 0x01), (0, 10, 0, 1, 0x22), (0, 10, 2040, 1, 0x12),
+                   (10, 10, 3, 2, 0x12)], dtype=gecko.FRAME_DTYPE)
+    off = np.arange(len(fr), dtype=np.uint64) * 2100
+    salts = sref.splitmix64_array(9, 0, len(fr))
+    o = hysteria_amd.SalamanderObfuscator(PSK, 0)
+    try:
+        out = torch.full((2100 * len(fr),), 0xA5, dtype=torch.uint8, device=gpu)
+        ws = torch.empty(gecko.workspace_size(len(fr)), dtype=torch.uint8, device=gpu)
+        gecko.encode_batch(o, msg=_dev(msg, gpu), frames=_dev(fr, gpu), salts=_dev(salts, gpu), pad_seed=5,
+                           out=out, out_off=_dev(off, gpu), workspace=ws)
+        got = out.cpu().numpy()
+    finally:
+        o.close()
+    exp = gref.encode_wire(PSK, msg.tobytes(), fr.tolist()[:1], salts[:1], 5)[0]
+    assert got[:len(exp)].tobytes() == exp
+    for i in (1, 2, 3):   # one chunk, index >= total, datagram over 2048 bytes: untouched
+        assert (got[2100 * i:2100 * (i + 1)] == 0xA5).all(), i
+    plain4 = gref.encode_frame(gref.Header(3, 2, 1, 2), msg[10:20].tobytes(), gref.pad_bytes(5, 4, 3))
+    exp4 = sref.obfuscate(PSK, plain4, int(salts[4]).to_bytes(8, "little"))
+    assert got[4 * 2100:4 * 2100 + len(exp4)].tobytes() == exp4
+
+
+def test_parse_batch_and_reassembly(gpu):
+    """Wire -> Salamander deobfuscate batch -> Gecko parse kernel -> host reassembly
+    (acceptChunk, gecko.go:195-250) in shuffled order: every message comes back."""
+    import torch
+    import hysteria_amd
+    from hysteria_amd import gecko
+    lens, msg = _messages(200, 11)
+    fr, off, total = gecko.plan_fragments(lens, 512, 1200, first_msg_id=0)
+    nf = len(fr)
+    salts = sref.splitmix64_array(6, 0, nf)
+    o = hysteria_amd.SalamanderObfuscator(PSK, 0)
+    try:
+        wire = torch.empty(total + 16, dtype=torch.uint8, device=gpu)
+        ws = torch.empty(gecko.workspace_size(nf), dtype=torch.uint8, device=gpu)
+        d_off = _dev(off, gpu)
+        gecko.encode_batch(o, msg=_dev(msg, gpu), frames=_dev(fr, gpu), salts=_dev(salts, gpu), pad_seed=77,
+                           out=wire, out_off=d_off, workspace=ws, n=nf)
+        wl = (13 + fr["chunk_len"].astype(np.uint32) + fr["pad_len"]).astype(np.uint32)
+        # append a short-header datagram, a dropped (8-byte) one and a malformed fragment
+        extra = [sref.obfuscate(PSK, b"\x40hello", b"\x01" * 8), b"\x02" * 8,
+                 sref.obfuscate(PSK, bytes([0x80, 1, 0x44, 0, 0]), b"\x03" * 8)]
+        tail = np.frombuffer(b"".join(extra), np.uint8)
+        wire_h = np.concatenate([wire.cpu().numpy()[:total], tail])
+        all_off = np.concatenate([off, total + np.cumsum([0] + [len(e) for e in extra[:-1]])]).astype(np.uint64)
+        all_len = np.concatenate([wl, [len(e) for e in extra]]).astype(np.uint32)
+        n = nf + len(extra)
+        d_wire = _dev(wire_h, gpu)
+        plain = torch.empty(len(wire_h) + 16, dtype=torch.uint8, device=gpu)
+        poff = torch.empty(n, dtype=torch.int64, device=gpu)
+        plen = torch.empty(n, dtype=torch.int32, device=gpu)
+        ws2 = torch.empty(hysteria_amd.workspace_size(n), dtype=torch.uint8, device=gpu)
+        o.deobfuscate_batch(d_wire, n, in_off=_dev(all_off, gpu).view(torch.int64),
+                            in_len=_dev(all_len, gpu).view(torch.int32), out=plain, out_cap=len(wire_h),
+                            out_off=poff, out_len=plen, workspace=ws2, workspace_bytes=ws2.numel())
+        parsed = torch.empty(n * 16, dtype=torch.uint8, device=gpu)
+        gecko.parse_batch(plain, poff, plen, n, parsed)
+        torch.cuda.synchronize()
+        pr = parsed.cpu().numpy().view(gecko.PARSED_DTYPE)
+        ph, ho, hl = plain.cpu().numpy(), poff.cpu().numpy().view(np.uint64), plen.cpu().numpy().view(np.uint32)
+    finally:
+        o.close()
+    assert int(pr[nf]["status"]) == gecko.PASS and int(pr[nf]["payload_len"]) == 6
+    assert int(pr[nf + 1]["status"]) == gecko.EMPTY          # 8-byte wire: Deobfuscate returns 0
+    assert int(pr[nf + 2]["status"]) == gecko.ERR_INVALID
+    for i in range(n):   # every datagram's classification matches the oracle's
+        d = ph[int(ho[i]):int(ho[i]) + int(hl[i])].tobytes()
+        kind = gref.parse(d)[0]
+        assert {gref.PASS: 0, gref.FRAGMENT: 1, gref.EMPTY: -22, gref.TRUNCATED: -20,
+                gref.INVALID: -21}[kind] == int(pr[i]["status"]), i
+    g = gecko.GeckoPacketConn(None)
+    order = list(range(nf))
+    random.Random(5).shuffle(order)
+    done = {}
+    for i in order:
+        r = pr[i]
+        po = int(ho[i]) + int(r["payload_off"])
+        payload = ph[po:po + int(r["payload_len"])].tobytes()
+        it = int(r["idx_total"])
+        h = gecko.FrameHeader(int(r["pad_len"]), int(r["msg_id"]), it >> 4, it & 0x0F)
+        # one source per message: shuffled fragments of 200 messages from ONE source
+        # would hit the per-source cap of 8 partial messages (gecko.go:209-212)
+        out = g.accept_chunk(("127.0.0.1", 1000 + h.msg_id), h, payload)
+        if out is not None:
+            done[h.msg_id] = out
+    g.close()
+    base = np.concatenate([[0], np.cumsum(lens)])
+    # msg ids wrap at 256: with 200 messages every id is unique
+    assert len(done) == len(lens)
+    for m in range(len(lens)):
+        assert done[m & 0xFF] == msg[base[m]:base[m + 1]].tobytes(), m
+
+
+def test_gecko_over_salamander_udp_loopback(gpu):
+    """WrapPacketConnGecko over a real UDP socket: short and long headers round-trip
+    (TestGeckoRoundTripShortHeader / LongHeader / SmallLongHeader)."""
+    from hysteria_amd import gecko
+    sa = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
+    sb = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
+    sa.bind(("127.0.0.1", 0))
+    sb.bind(("127.0.0.1", 0))
+    ga = gecko.wrap_packet_conn_gecko(sa, gecko.GeckoOptions(b"test"))
+    gb = gecko.wrap_packet_conn_gecko(sb, gecko.GeckoOptions(b"test"))
+    try:
+        gb.inner.settimeout(5.0)
+        for size, first in [(400, 0x40), (1200, 0xC0), (1, 0xC0), (27, 0xC0), (128, 0xC0), (2000, 0xC0)]:
+            p = bytearray(random.Random(size).randbytes(size))
+            p[0] = first
+            assert ga.write_to(bytes(p), sb.getsockname()) == size
+            got, src = gb.read_from(4096)
+            assert got == bytes(p), size
+            assert src[1] == sa.getsockname()[1]
+    finally:
+        ga.close()
+        gb.close()
