@@ -30,6 +30,7 @@
 #define __global__
 #define __device__
 #define __host__
+#define __constant__
 #define __forceinline__ inline
 #define __launch_bounds__(...)
 #define __shared__ static

@@ -193,6 +193,29 @@ def case_gecko(n_msgs, seed):
     assert int(parsed[0]["status"]) == gecko.ERR_INVALID
 
 
+def case_punch(n, m, seed):
+    from hysteria_amd import realm
+    from oracle import realm_ref as rref
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from punch_cases import punch_batch
+    pk, atts, metas = punch_batch(n, m, seed)
+    buf = np.frombuffer(b"".join(pk) + bytes(16), np.uint8).copy()
+    off = np.concatenate([[0], np.cumsum([len(x) for x in pk])[:-1]]).astype(np.uint64)
+    ln = np.array([len(x) for x in pk], np.uint32)
+    match = np.full(n, -7, np.int32)
+    ty = np.zeros(n, np.uint8)
+    pad = np.zeros(n, np.uint32)
+    mt = realm.PunchMatcher(metas)
+    p = lambda a: a.ctypes.data  # noqa: E731
+    mt.match_batch(p(buf), p(off), p(ln), n, p(match), p(ty), p(pad), attempts=p(mt.attempts), stream=0)
+    hits = 0
+    for i, x in enumerate(pk):
+        j, t, pd = rref.match(x, atts)
+        assert (int(match[i]), int(ty[i]) if j >= 0 else 0, int(pad[i])) == (j, t, pd), (i, int(match[i]), j)
+        hits += j >= 0
+    assert 0 < hits < n
+
+
 if __name__ == "__main__":
     lib = _lib.load()
     which = sys.argv[1]
@@ -211,6 +234,8 @@ if __name__ == "__main__":
         case_slotted_far(args[0], args[1], args[2], bool(args[3]))
     elif which == "ragged":
         case_ragged(args[0], args[1], args[2], bool(args[3]), ["packed", "slotted"][args[4]])
+    elif which == "punch":
+        case_punch(args[0], args[1], args[2])
     elif which == "gecko":
         case_gecko(args[0], args[1])
     print("ok", which, args)

@@ -48,6 +48,7 @@ CASES = [
     ("far", "200 300 15 1", "8"),        # workgroup bases beyond 2^31
     ("far", "200 300 15 0", "8"),
     ("gecko", "40 7", "2"),              # Gecko frame encode + parse kernels (gecko.hip)
+    ("punch", "300 5 3", "2"),           # realm punch matcher (realm.hip)
 ]
 
 
