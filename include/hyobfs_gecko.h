@@ -95,8 +95,9 @@ typedef struct hyobfs_gecko_batch {
     const uint8_t* msg;                  /* message bytes (device) */
     const hyobfs_gecko_frame* frames;    /* n frames (device) */
     const uint64_t* salts;               /* n Salamander salts (device), as hyobfs_batch.salts */
-    uint64_t pad_seed;                   /* pad byte j of frame i = byte i*2048 + j of the
-                                            little-endian SplitMix64(pad_seed) stream */
+    uint64_t pad_seed;                   /* pad byte j of frame i = byte i*2048 + 5 + j (its
+                                            plaintext position) of the little-endian
+                                            SplitMix64(pad_seed) stream */
     uint8_t* out;                        /* device */
     const uint64_t* out_off;             /* frame i's wire datagram at out + out_off[i] (device);
                                             its length is 8 + 5 + pad_len + chunk_len */

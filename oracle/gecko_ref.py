@@ -14,7 +14,7 @@ Restated from the reference (paths relative to apernet/hysteria):
 * ``extras/obfs/gecko.go:170-193``      -- ``ReadFrom``: ``n <= 0`` skipped, top bit clear passed through
 
 Randomness (crypto/rand in the reference) is an explicit input here: pad bytes
-come from the SplitMix64 stream of ``include/hyobfs_gecko.h`` (byte ``i*2048+j``
+come from the SplitMix64 stream of ``include/hyobfs_gecko.h`` (byte ``i*2048+5+j``
 of stream ``pad_seed`` for pad byte *j* of frame *i*), so device output is
 deterministic and comparable byte for byte.  The reference's own tests
 (``gecko_frame_test.go``, ``gecko_test.go``) check round trips, header fields,
@@ -94,7 +94,8 @@ def split_chunks(msg_len: int, chunks: int) -> list[tuple[int, int]]:
 
 
 def pad_bytes(pad_seed: int, frame: int, n: int) -> bytes:
-    return sref.stream_bytes(pad_seed, frame * BUFFER_SIZE, n)
+    """Pad bytes of frame i: bytes i*2048 + 5 + j (plaintext positions) of the stream."""
+    return sref.stream_bytes(pad_seed, frame * BUFFER_SIZE + HEADER_LEN, n)
 
 
 def encode_wire(psk: bytes, msg: bytes, frames, salts, pad_seed: int) -> list[bytes]:
