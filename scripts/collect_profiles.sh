@@ -12,7 +12,7 @@ for c in FETCH_SIZE WRITE_SIZE; do
     python3 "$R/scripts/prof_one.py" uniform 5 > "$O/pmc_$c.log" 2>&1 || { echo "pmc $c failed"; exit 1; }
 done
 python3 "$R/scripts/pmc_traffic.py" "$O" > "$O/pmc_traffic.json" || exit 1
-cp "$O/pmc_traffic.json" "$R/profiles/pmc_traffic.json"
+cp "$O/pmc_traffic.json" "$R/profiles/pmc_traffic.json"   # box copy only: also copy gpurun_out/profiles/pmc_traffic.json into profiles/ here
 # 2. kernel trace + stats of the bench command itself
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/kt" -o run -- \
   python3 "$R/bench.py" --steps 20 --warmup 5 --no-cpu-baseline --no-parity > "$O/kt_bench.log" 2>&1 || { echo "kt failed"; exit 1; }
