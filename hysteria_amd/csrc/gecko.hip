@@ -1,17 +1,18 @@
 // gecko.hip -- Gecko framing kernels (include/hyobfs_gecko.h).
 //
-// Encode: 16 lanes per frame, four frames per wavefront.  The wire datagram of frame f is
+// Encode: one wavefront per group of 64 frames.  The wire datagram of frame f is
 //     salt(8) || (hdr(5) || pad || chunk) ^ key_f[i % 32]
-// (gecko_frame.go:39-61 encodeFrame, then salamander.go:59-72 Obfuscate).  Lane
-// l of a frame handles plaintext windows of 16 bytes at 16l, 16(l+16), ..., four
-// in flight (loads first, then stores): a window inside
-// the chunk is one unaligned 16-byte load, one inside the padding is two
-// SplitMix64 words, a window across header / padding / chunk merges the
-// three under byte masks, and each leaves as one 16-byte store (the frame's last
-// partial window as bytes).  The
-// key half a lane needs is the same on every pass (window index parity = lane
-// parity), so it is loaded once.  Keys come from keys_kernel (salamander.hip)
-// into the workspace.
+// (gecko_frame.go:39-61 encodeFrame, then salamander.go:59-72 Obfuscate).  Lane l
+// loads frame l's record, offsets, salt and key once into LDS (and writes the
+// salt); a wave scan numbers the group's 16-byte plaintext windows, and the 64
+// lanes sweep the interior ones, several per lane in flight (loads first, then
+// stores), finding each window's frame by a 6-step LDS binary search: a window
+// inside the chunk is one unaligned 16-byte load, one inside the padding is two
+// SplitMix64 words (pad byte at plaintext position q is stream byte f*2048 + q),
+// each leaves as one 16-byte store.  Then lane l merges frame l's few edge windows
+// (header, padding/chunk seam, frame end) under byte masks; keeping them out of
+// the sweep keeps its lanes on the same path.  Keys come from
+// keys_kernel (salamander.hip) into the workspace.
 //
 // Parse: one thread per deobfuscated datagram, the checks of ReadFrom
 // (gecko.go:170-193) and decodeFrame (gecko_frame.go:65-86) in their order.
@@ -40,90 +41,152 @@ __device__ __forceinline__ gk_u128 gk_mask(uint32_t lo, uint32_t hi) {   // byte
     return m << (8 * lo);
 }
 
-#ifndef HY_GK_FPW
-#define HY_GK_FPW 8
-#endif
 #ifndef HY_GK_U
-#define HY_GK_U 1
+#define HY_GK_U 4
 #endif
-constexpr int kGkFramesPerWave = HY_GK_FPW;       // frames per wavefront
-constexpr int kGkLanes = 64 / kGkFramesPerWave;   // lanes per frame
-constexpr int kGkU = HY_GK_U;                     // windows per lane in flight
+constexpr int kGkU = HY_GK_U;   // windows per lane in flight
+
+struct GeckoGroup {             // one wave's 64 frames, in LDS
+    uint64_t out_off[64];       // wire datagram start
+    uint64_t chunk_off[64];
+    uint64_t hdr[64];           // the 5 header bytes, little-endian in the low bytes
+    uint32_t wstart[65];        // first plaintext window of the frame (exclusive scan), [64] = total
+    uint32_t hp_plain[64];      // chunk start (low 16 bits) | plaintext length (high 16 bits)
+    gk_u128 key[128];           // the frame's key, two halves
+};
 
 __global__ __launch_bounds__(256) void gecko_encode_kernel(hyobfs_gecko_batch B) {
-    const uint32_t lane = threadIdx.x & 63, sl = lane % kGkLanes;
-    const uint64_t f = ((uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * kGkFramesPerWave + lane / kGkLanes;
-    if (f >= B.n) return;
-    const hyobfs_gecko_frame fr = B.frames[f];
-    const uint32_t total = fr.idx_total & 0x0f, idx = fr.idx_total >> 4;
-    const uint32_t hp = HYOBFS_GECKO_HEADER_LEN + fr.pad_len;   // chunk start in the plaintext
-    const uint32_t plain = hp + fr.chunk_len;
-    if (total < HYOBFS_GECKO_MIN_CHUNKS || total > HYOBFS_GECKO_MAX_CHUNKS || idx >= total ||
-        HYOBFS_SALT_LEN + plain > HYOBFS_GECKO_BUFFER_SIZE)
-        return;   // not a frame writeFragmented can produce: skipped
-    // lane handles plaintext windows [16k, 16k+16), k = sl, sl+16, ...: always the same key half
-    gk_u128 kh;
-    __builtin_memcpy(&kh, static_cast<const uint8_t*>(B.workspace) + 32 * f + 16 * (sl & 1), 16);
-    uint8_t* __restrict__ out = B.out + B.out_off[f];
-    if (sl == 0) {
-        const uint64_t salt = B.salts[f];
-        __builtin_memcpy(out, &salt, HYOBFS_SALT_LEN);
+    __shared__ GeckoGroup gg[4];
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    GeckoGroup& G = gg[wid];
+    const uint64_t f0 = ((uint64_t)blockIdx.x * 4 + wid) * 64;
+    if (f0 >= B.n) return;
+    // ---- 1. lane l: frame f0 + l's record, offsets, salt and key into LDS
+    const uint64_t f = f0 + lane;
+    uint32_t nwin = 0;
+    if (f < B.n) {
+        const hyobfs_gecko_frame fr = B.frames[f];
+        const uint32_t total = fr.idx_total & 0x0f, idx = fr.idx_total >> 4;
+        const uint32_t hp = HYOBFS_GECKO_HEADER_LEN + fr.pad_len, plain = hp + fr.chunk_len;
+        if (total >= HYOBFS_GECKO_MIN_CHUNKS && total <= HYOBFS_GECKO_MAX_CHUNKS && idx < total &&
+            HYOBFS_SALT_LEN + plain <= HYOBFS_GECKO_BUFFER_SIZE) {   // else: skipped, nothing written
+            nwin = (plain + 15) >> 4;
+            const uint64_t oo = B.out_off[f];
+            G.out_off[lane] = oo;
+            G.chunk_off[lane] = fr.chunk_off;
+            G.hdr[lane] = (uint64_t)HYOBFS_GECKO_FLAG_FRAGMENT | (uint64_t)fr.msg_id << 8 |
+                          (uint64_t)fr.idx_total << 16 | (uint64_t)(fr.pad_len >> 8) << 24 |
+                          (uint64_t)(fr.pad_len & 0xff) << 32;
+            G.hp_plain[lane] = hp | plain << 16;
+            const uint8_t* kp = static_cast<const uint8_t*>(B.workspace) + 32 * f;
+            gk_u128 k0, k1;
+            __builtin_memcpy(&k0, kp, 16);
+            __builtin_memcpy(&k1, kp + 16, 16);
+            G.key[2 * lane] = k0;
+            G.key[2 * lane + 1] = k1;
+            const uint64_t salt = B.salts[f];
+            __builtin_memcpy(B.out + oo, &salt, HYOBFS_SALT_LEN);
+        }
     }
-    uint8_t* __restrict__ po = out + HYOBFS_SALT_LEN;
-    const uint8_t* __restrict__ chunk = B.msg + fr.chunk_off;
-    const uint64_t pad0 = f * HYOBFS_GECKO_BUFFER_SIZE;   // this frame's window of the pad stream
-    // 0x80 | msgID | idx<<4|total | padLen big-endian, as the low 5 bytes of a window
-    const gk_u128 hdr = (gk_u128)HYOBFS_GECKO_FLAG_FRAGMENT | (gk_u128)fr.msg_id << 8 | (gk_u128)fr.idx_total << 16 |
-                        (gk_u128)(fr.pad_len >> 8) << 24 | (gk_u128)(fr.pad_len & 0xff) << 32;
-    // pad byte at plaintext position q is byte pad0 + q of the stream: a window's 16
-    // bytes are exactly two SplitMix64 words (pad0 and p are multiples of 16)
-    auto stream16 = [&](uint32_t p) -> gk_u128 {
+    uint32_t inc = nwin;   // inclusive scan of window counts
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(inc, d, 64);
+        if (lane >= (uint32_t)d) inc += y;
+    }
+    G.wstart[lane] = inc - nwin;
+    if (lane == 63) G.wstart[64] = inc;
+    hy_wave_sync();
+    const uint32_t tw = __builtin_amdgcn_readfirstlane(G.wstart[64]);
+    // A window is interior when it lies inside the padding or inside the chunk; the
+    // sweep does only those (no divergent byte merging), lane l then finishes frame
+    // l's few edge windows (header, padding/chunk seam, the frame's end).
+    auto interior = [](uint32_t p, uint32_t hp, uint32_t plain) {
+        return (p >= hp && p + 16 <= plain) || (p >= HYOBFS_GECKO_HEADER_LEN && p + 16 <= hp);
+    };
+    auto pad16 = [&](uint32_t k, uint32_t p) -> gk_u128 {   // pad stream at plaintext [p, p+16) of frame f0+k
 #ifdef HY_X_NOPAD   // ablation builds only (timing experiments; wrong output)
-        return (gk_u128)(pad0 + p);
+        return (gk_u128)(f0 + k + p);
 #else
-        const uint64_t w = (pad0 + p) >> 3;
+        const uint64_t w = ((f0 + k) * HYOBFS_GECKO_BUFFER_SIZE + p) >> 3;
         return (gk_u128)gk_sm64(B.pad_seed, w + 1) << 64 | gk_sm64(B.pad_seed, w);
 #endif
     };
-    auto window = [&](uint32_t p) -> gk_u128 {   // plaintext bytes [p, p+16) ^ key, p < plain
-        const uint32_t e = min(p + 16, plain);
-        gk_u128 v = 0;
-        if (p == 0) v = hdr & gk_mask(0, min(e, (uint32_t)HYOBFS_GECKO_HEADER_LEN));
-        const uint32_t plo = max(p, (uint32_t)HYOBFS_GECKO_HEADER_LEN), phi = min(e, hp);
-        if (plo < phi) {   // padding bytes of the window
-            v |= stream16(p) & gk_mask(plo - p, phi - p);
+    auto store = [&](uint32_t k, uint32_t p, uint32_t plain, gk_u128 v) {
+        uint8_t* __restrict__ po = B.out + G.out_off[k] + HYOBFS_SALT_LEN;
+        if (p + 16 <= plain) {
+#ifdef HY_X_ALIGNST   // ablation builds only (timing experiments; wrong output)
+            gk_store16u((uint8_t*)((uintptr_t)(po + p) & ~(uintptr_t)15), v);
+#else
+            gk_store16u(po + p, v);
+#endif
+        } else {   // the frame's last partial window
+            for (uint32_t j = p; j < plain; ++j) po[j] = (uint8_t)(v >> (8 * (j - p)));
         }
-        const uint32_t clo = max(p, hp);
-        if (clo < e) {     // chunk bytes of the window
-            gk_u128 X = 0;
-            if (p >= hp && p + 16 <= plain) {
-                X = gk_load16u(chunk + (p - hp));
-            } else if (fr.chunk_len >= 16) {   // first or last window of the chunk: one in-bounds load, shifted
-                X = p < hp ? gk_load16u(chunk) << (8 * (hp - p))
-                           : gk_load16u(chunk + (fr.chunk_len - 16)) >> (8 * (p + 16 - plain));
-            } else {
-                for (uint32_t j = clo; j < e; ++j) X |= (gk_u128)chunk[j - hp] << (8 * (j - p));
-            }
-            v |= X & gk_mask(clo - p, e - p);
-        }
-        return v ^ kh;
     };
-    constexpr uint32_t STEP = 16 * kGkLanes;   // bytes per pass of the frame's lanes
-    for (uint32_t p0 = 16 * sl; p0 < plain; p0 += STEP * kGkU) {
+    // ---- 2. sweep: window t belongs to the last frame whose first window is <= t
+    for (uint32_t t0 = lane; t0 < tw; t0 += 64 * kGkU) {
         gk_u128 v[kGkU];
+        uint32_t kk[kGkU], pp[kGkU];
+        bool ok[kGkU];
 #pragma unroll
         for (int u = 0; u < kGkU; ++u) {   // all windows' loads first
-            const uint32_t p = p0 + STEP * u;
-            v[u] = p < plain ? window(p) : (gk_u128)0;
+            const uint32_t t = t0 + 64 * u;
+            uint32_t q = 0;
+            if (t < tw) {
+#pragma unroll
+                for (uint32_t step = 32; step; step >>= 1) q = (G.wstart[q + step] <= t) ? q + step : q;
+            }
+            const uint32_t wi = t - G.wstart[q], p = 16 * wi;
+            const uint32_t hpl = G.hp_plain[q], hp = hpl & 0xffff, plain = hpl >> 16;
+            kk[u] = q;
+            pp[u] = p;
+            ok[u] = t < tw && interior(p, hp, plain);
+            v[u] = 0;
+            if (ok[u]) {
+                v[u] = p >= hp ? gk_load16u(B.msg + G.chunk_off[q] + (p - hp)) : pad16(q, p);
+                v[u] ^= G.key[2 * q + (wi & 1)];
+            }
         }
 #pragma unroll
-        for (int u = 0; u < kGkU; ++u) {
-            const uint32_t p = p0 + STEP * u;
-            if (p + 16 <= plain) {
-                gk_store16u(po + p, v[u]);
-            } else if (p < plain) {   // the frame's last partial window
-                for (uint32_t j = p; j < plain; ++j) po[j] = (uint8_t)(v[u] >> (8 * (j - p)));
+        for (int u = 0; u < kGkU; ++u)
+            if (ok[u]) store(kk[u], pp[u], 0xFFFFFFFFu, v[u]);
+    }
+    // ---- 3. edge windows of frame `lane`: header window, the window holding the
+    // padding/chunk seam and the next one (short chunks), and the last window
+    if (nwin) {
+        const uint32_t k = lane;
+        const uint32_t hpl = G.hp_plain[k], hp = hpl & 0xffff, plain = hpl >> 16;
+        const uint8_t* __restrict__ chunk = B.msg + G.chunk_off[k];
+        const uint32_t cand[4] = {0u, hp >> 4, (hp >> 4) + 1, nwin - 1};
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const uint32_t wi = cand[c];
+            bool dup = wi >= nwin;
+#pragma unroll
+            for (int d = 0; d < c; ++d) dup = dup || cand[d] == wi;
+            const uint32_t p = 16 * wi;
+            if (dup || interior(p, hp, plain)) continue;
+            const uint32_t e = min(p + 16, plain);
+            gk_u128 v = 0;
+            if (p == 0) v = (gk_u128)G.hdr[k] & gk_mask(0, min(e, (uint32_t)HYOBFS_GECKO_HEADER_LEN));
+            const uint32_t plo = max(p, (uint32_t)HYOBFS_GECKO_HEADER_LEN), phi = min(e, hp);
+            if (plo < phi) v |= pad16(k, p) & gk_mask(plo - p, phi - p);
+            const uint32_t clo = max(p, hp);
+            if (clo < e) {   // chunk bytes
+                const uint32_t clen = plain - hp;
+                gk_u128 X = 0;
+                if (p >= hp && p + 16 <= plain) {
+                    X = gk_load16u(chunk + (p - hp));
+                } else if (clen >= 16) {   // first or last window of the chunk: one in-bounds load, shifted
+                    X = p < hp ? gk_load16u(chunk) << (8 * (hp - p)) : gk_load16u(chunk + (clen - 16)) >> (8 * (p + 16 - plain));
+                } else {
+                    for (uint32_t j = clo; j < e; ++j) X |= (gk_u128)chunk[j - hp] << (8 * (j - p));
+                }
+                v |= X & gk_mask(clo - p, e - p);
             }
+            store(k, p, plain, v ^ G.key[2 * k + (wi & 1)]);
         }
     }
 }
@@ -166,8 +229,7 @@ hipError_t launch_gecko_encode(const KeyParams& k, const hyobfs_gecko_batch& b, 
     if (b.n == 0) return hipSuccess;
     hipError_t e = launch_keys(k, b.salts, static_cast<uint8_t*>(b.workspace), b.n, s);
     if (e != hipSuccess) return e;
-    const uint64_t per_block = 4 * kGkFramesPerWave;
-    hipLaunchKernelGGL(gecko_encode_kernel, dim3((uint32_t)((b.n + per_block - 1) / per_block)), dim3(256), 0, s, b);
+    hipLaunchKernelGGL(gecko_encode_kernel, dim3((uint32_t)((b.n + 255) / 256)), dim3(256), 0, s, b);
     return hipGetLastError();
 }
 
