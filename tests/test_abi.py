@@ -63,3 +63,30 @@ def test_batch_struct_layout_matches_header(tmp_path):
     vals = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()]
     py = [getattr(_lib.HyobfsBatch, f).offset for f in fields] + [ctypes.sizeof(_lib.HyobfsBatch)]
     assert vals == py
+
+
+def _c_layout(tmp_path, header, ctype, cfields):
+    src = tmp_path / f"probe_{ctype}.c"
+    body = "\n".join(f'printf("%zu\\n", offsetof({ctype}, {c}));' for c in cfields)
+    src.write_text(f'#include <stdio.h>\n#include <stddef.h>\n#include "{header}"\nint main(void){{\n'
+                   + body + f'\nprintf("%zu\\n", sizeof({ctype}));return 0;}}\n')
+    exe = tmp_path / f"probe_{ctype}"
+    subprocess.run(["gcc", "-std=c11", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
+    return [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()]
+
+
+def test_gecko_and_realm_struct_layouts_match_headers(tmp_path):
+    """The Python mirrors of hyobfs_gecko.h / hyobfs_realm.h structs (ctypes and numpy
+    records) have the C offsets and sizes."""
+    from hysteria_amd import gecko, realm
+    for ct, cls in (("hyobfs_gecko_header", gecko.HyobfsGeckoHeader), ("hyobfs_gecko_batch", gecko.HyobfsGeckoBatch),
+                    ("hyobfs_punch_attempt", realm.HyobfsPunchAttempt)):
+        names = [f[0] for f in cls._fields_]
+        header = "hyobfs_realm.h" if ct.startswith("hyobfs_punch") else "hyobfs_gecko.h"
+        vals = _c_layout(tmp_path, header, ct, names)
+        assert vals == [getattr(cls, f).offset for f in names] + [ctypes.sizeof(cls)], ct
+    for ct, dt in (("hyobfs_gecko_frame", gecko.FRAME_DTYPE), ("hyobfs_gecko_parsed", gecko.PARSED_DTYPE),
+                   ("hyobfs_punch_attempt", realm.ATTEMPT_DTYPE)):
+        header = "hyobfs_realm.h" if ct.startswith("hyobfs_punch") else "hyobfs_gecko.h"
+        vals = _c_layout(tmp_path, header, ct, list(dt.names))
+        assert vals == [dt.fields[n][1] for n in dt.names] + [dt.itemsize], ct
