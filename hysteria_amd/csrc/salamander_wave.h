@@ -182,9 +182,19 @@ __device__ __forceinline__ void group_contrib(const GroupBuf& G, const uint8_t* 
 
 // Streamed input of the wave kernel: read once, non-temporal (measured faster
 // here; the persistent kernel keeps HY_NT_LOADS).
+#ifndef HY_WAVE_NT_LOADS
+#define HY_WAVE_NT_LOADS 1
+#endif
 __device__ __forceinline__ u128 load16_nt(const uint8_t* p) {
-#ifdef HYOBFS_EMULATE
+#if defined(HYOBFS_EMULATE)
     return load16u(p);
+#elif !HY_WAVE_NT_LOADS
+    typedef uint32_t v4u __attribute__((ext_vector_type(4), aligned(4)));
+    typedef const __attribute__((address_space(1))) v4u gv4u;
+    const v4u v = *(gv4u*)(p);
+    u128 r;
+    __builtin_memcpy(&r, &v, 16);
+    return r;
 #else
     // explicitly global: a generic pointer lets the compiler merge this load
     // with the sweep's LDS read of a parked chunk into one (slow) flat load
