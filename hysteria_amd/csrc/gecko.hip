@@ -6,23 +6,24 @@
 // loads frame l's record, offsets, salt and key once into LDS (and writes the
 // salt); a wave scan numbers the group's 16-byte plaintext windows, and the 64
 // lanes sweep the interior ones, several per lane in flight (loads first, then
-// stores), finding each window's frame by a 6-step LDS binary search: a window
+// stores), each lane walking its window's frame forward through the LDS scan: a window
 // inside the chunk is one unaligned 16-byte load, one inside the padding is two
 // SplitMix64 words (pad byte at plaintext position q is stream byte f*2048 + q),
 // each leaves as one 16-byte store.  Then lane l merges frame l's few edge windows
 // (header, padding/chunk seam, frame end) under byte masks; keeping them out of
-// the sweep keeps its lanes on the same path.  Keys come from
-// keys_kernel (salamander.hip) into the workspace.
+// the sweep keeps its lanes on the same path.  Lane l hashes frame l's key
+// (BLAKE2b-256, salamander_device.h) in registers in step 1, so the hash overlaps
+// other waves' sweeps (a separate keys_kernel pass via the workspace was 15 % slower).
 //
 // Parse: one thread per deobfuscated datagram, the checks of ReadFrom
 // (gecko.go:170-193) and decodeFrame (gecko_frame.go:65-86) in their order.
 #include "kernels.h"
+#include "salamander_device.h"
 #include "../../include/hyobfs_gecko.h"
 
 namespace hyobfs {
 
-__device__ __forceinline__ uint64_t gk_sm64(uint64_t seed, uint64_t k) {   // SplitMix64 output k
-    uint64_t z = seed + (k + 1) * 0x9e3779b97f4a7c15ull;
+__device__ __forceinline__ uint64_t gk_mix64(uint64_t z) {   // SplitMix64 finaliser
     z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
     z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
     return z ^ (z >> 31);
@@ -55,7 +56,12 @@ struct GeckoGroup {             // one wave's 64 frames, in LDS
     gk_u128 key[128];           // the frame's key, two halves
 };
 
-__global__ __launch_bounds__(256) void gecko_encode_kernel(hyobfs_gecko_batch B) {
+#ifdef HY_GK_WPE   // A/B builds only: register cap for the fused hash
+#define HY_GK_ATTR __attribute__((amdgpu_waves_per_eu(HY_GK_WPE)))
+#else
+#define HY_GK_ATTR
+#endif
+__global__ __launch_bounds__(256) HY_GK_ATTR void gecko_encode_kernel(KeyParams K, hyobfs_gecko_batch B) {
     __shared__ GeckoGroup gg[4];
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -79,13 +85,19 @@ __global__ __launch_bounds__(256) void gecko_encode_kernel(hyobfs_gecko_batch B)
                           (uint64_t)fr.idx_total << 16 | (uint64_t)(fr.pad_len >> 8) << 24 |
                           (uint64_t)(fr.pad_len & 0xff) << 32;
             G.hp_plain[lane] = hp | plain << 16;
+            const uint64_t salt = B.salts[f];
+#ifdef HY_GK_KEYS_KERNEL   // A/B builds only: keys from keys_kernel via the workspace
             const uint8_t* kp = static_cast<const uint8_t*>(B.workspace) + 32 * f;
             gk_u128 k0, k1;
             __builtin_memcpy(&k0, kp, 16);
             __builtin_memcpy(&k1, kp + 16, 16);
+#else   // keyLocked (salamander.go:88-91) in registers; the hash overlaps other waves' sweeps
+            uint64_t kw[4];
+            salamander_key(K, salt, kw);
+            const gk_u128 k0 = (gk_u128)kw[1] << 64 | kw[0], k1 = (gk_u128)kw[3] << 64 | kw[2];
+#endif
             G.key[2 * lane] = k0;
             G.key[2 * lane + 1] = k1;
-            const uint64_t salt = B.salts[f];
             __builtin_memcpy(B.out + oo, &salt, HYOBFS_SALT_LEN);
         }
     }
@@ -110,7 +122,8 @@ __global__ __launch_bounds__(256) void gecko_encode_kernel(hyobfs_gecko_batch B)
         return (gk_u128)(f0 + k + p);
 #else
         const uint64_t w = ((f0 + k) * HYOBFS_GECKO_BUFFER_SIZE + p) >> 3;
-        return (gk_u128)gk_sm64(B.pad_seed, w + 1) << 64 | gk_sm64(B.pad_seed, w);
+        const uint64_t z0 = B.pad_seed + (w + 1) * 0x9e3779b97f4a7c15ull;   // SplitMix64 outputs w and w + 1
+        return (gk_u128)gk_mix64(z0 + 0x9e3779b97f4a7c15ull) << 64 | gk_mix64(z0);
 #endif
     };
     auto store = [&](uint32_t k, uint32_t p, uint32_t plain, gk_u128 v) {
@@ -125,7 +138,11 @@ __global__ __launch_bounds__(256) void gecko_encode_kernel(hyobfs_gecko_batch B)
             for (uint32_t j = p; j < plain; ++j) po[j] = (uint8_t)(v >> (8 * (j - p)));
         }
     };
-    // ---- 2. sweep: window t belongs to the last frame whose first window is <= t
+    // ---- 2. sweep: window t belongs to the last frame whose first window is <= t.
+    // A lane's windows only move forward (t0 + 64 u), so its frame index q does too:
+    // it steps over the frames started since its previous window (one or two LDS
+    // reads for frames of >= 32 windows) instead of a fresh 6-step search.
+    uint32_t q = 0;
     for (uint32_t t0 = lane; t0 < tw; t0 += 64 * kGkU) {
         gk_u128 v[kGkU];
         uint32_t kk[kGkU], pp[kGkU];
@@ -133,11 +150,16 @@ __global__ __launch_bounds__(256) void gecko_encode_kernel(hyobfs_gecko_batch B)
 #pragma unroll
         for (int u = 0; u < kGkU; ++u) {   // all windows' loads first
             const uint32_t t = t0 + 64 * u;
-            uint32_t q = 0;
+#ifdef HY_GK_BSEARCH   // A/B builds only: the per-window binary search
+            q = 0;
             if (t < tw) {
 #pragma unroll
                 for (uint32_t step = 32; step; step >>= 1) q = (G.wstart[q + step] <= t) ? q + step : q;
             }
+#else
+            if (t < tw)   // wstart[64] = tw > t stops the walk at frame 63
+                while (G.wstart[q + 1] <= t) ++q;
+#endif
             const uint32_t wi = t - G.wstart[q], p = 16 * wi;
             const uint32_t hpl = G.hp_plain[q], hp = hpl & 0xffff, plain = hpl >> 16;
             kk[u] = q;
@@ -227,9 +249,11 @@ __global__ __launch_bounds__(256) void gecko_parse_kernel(const uint8_t* in, con
 
 hipError_t launch_gecko_encode(const KeyParams& k, const hyobfs_gecko_batch& b, hipStream_t s) {
     if (b.n == 0) return hipSuccess;
+#ifdef HY_GK_KEYS_KERNEL
     hipError_t e = launch_keys(k, b.salts, static_cast<uint8_t*>(b.workspace), b.n, s);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(gecko_encode_kernel, dim3((uint32_t)((b.n + 255) / 256)), dim3(256), 0, s, b);
+#endif
+    hipLaunchKernelGGL(gecko_encode_kernel, dim3((uint32_t)((b.n + 255) / 256)), dim3(256), 0, s, k, b);
     return hipGetLastError();
 }
 

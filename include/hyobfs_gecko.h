@@ -101,7 +101,8 @@ typedef struct hyobfs_gecko_batch {
     uint8_t* out;                        /* device */
     const uint64_t* out_off;             /* frame i's wire datagram at out + out_off[i] (device);
                                             its length is 8 + 5 + pad_len + chunk_len */
-    void* workspace;                     /* >= hyobfs_gecko_workspace_size(n) bytes (device) */
+    void* workspace;                     /* >= hyobfs_gecko_workspace_size(n) bytes (device);
+                                            reserved: the kernel derives keys in registers */
     uint64_t workspace_bytes;
 } hyobfs_gecko_batch;
 
