@@ -253,6 +253,8 @@ hipError_t launch_gecko_encode(const KeyParams& k, const hyobfs_gecko_batch& b, 
     hipError_t e = launch_keys(k, b.salts, static_cast<uint8_t*>(b.workspace), b.n, s);
     if (e != hipSuccess) return e;
 #endif
+    // (Instantiating per salt word as the wave kernel does cuts 96 -> 60 VGPRs, 5 -> 8
+    // waves/SIMD, and measured 4 % slower: profiles/r01_ab_gecko/.)
     hipLaunchKernelGGL(gecko_encode_kernel, dim3((uint32_t)((b.n + 255) / 256)), dim3(256), 0, s, k, b);
     return hipGetLastError();
 }

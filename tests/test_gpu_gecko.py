@@ -55,6 +55,33 @@ def test_encode_batch_vs_oracle(gpu, n_msgs, lo, hi):
         assert w >= lo or 13 + int(fr[i]["chunk_len"]) > hi
 
 
+@pytest.mark.parametrize("psk_len", [4, 9, 24, 57, 100, 113, 119, 120, 121, 127, 128, 200, 300])
+def test_encode_batch_psk_lengths(gpu, psk_len):
+    """The encode kernel hashes keys in registers, instantiated per salt word of the
+    device block (salt_pos >> 3): PSK lengths cover every word, the two-block chain
+    (salt_pos 121..127) and multi-block prefixes."""
+    import torch
+    import hysteria_amd
+    from hysteria_amd import gecko
+    psk = bytes((7 * i + psk_len) & 0xff for i in range(psk_len))
+    lens, msg = _messages(40, psk_len)
+    fr, off, total = gecko.plan_fragments(lens, 512, 1200, first_msg_id=psk_len)
+    nf = len(fr)
+    salts = sref.splitmix64_array(psk_len, 0, nf)
+    o = hysteria_amd.SalamanderObfuscator(psk, 0)
+    try:
+        out = torch.zeros((total,), dtype=torch.uint8, device=gpu)
+        ws = torch.empty(gecko.workspace_size(nf), dtype=torch.uint8, device=gpu)
+        gecko.encode_batch(o, msg=_dev(msg, gpu), frames=_dev(fr, gpu), salts=_dev(salts, gpu), pad_seed=psk_len,
+                           out=out, out_off=_dev(off, gpu), workspace=ws, n=nf)
+        got = out.cpu().numpy()
+    finally:
+        o.close()
+    exp = gref.encode_wire(psk, msg.tobytes(), fr.tolist(), salts, psk_len)
+    for i in range(nf):
+        assert got[int(off[i]):int(off[i]) + len(exp[i])].tobytes() == exp[i], i
+
+
 def test_encode_batch_skips_impossible_frames(gpu):
     import torch
     import hysteria_amd
