@@ -252,7 +252,13 @@ __global__ __launch_bounds__(kGroup* kWavesPerBlock, HY_WAVE_MIN_WAVES) void sal
     // on neighbouring runs and the chip sweeps memory in address order.
     const uint32_t rl = B.run_log2, RUN = 1u << rl;
     const uint64_t Wt = (uint64_t)gridDim.x * kWavesPerBlock;
+#ifdef HY_XCD_REMAP   // A/B builds only: consecutive logical blocks on one XCD (bijective remap)
+    const uint32_t nwg = gridDim.x, ob = blockIdx.x, xq = nwg / 8, xr = nwg % 8, xcd = ob % 8;
+    const uint32_t lb = (xcd < xr ? xcd * (xq + 1) : xr * (xq + 1) + (xcd - xr) * xq) + ob / 8;
+    const uint64_t w = (uint64_t)lb * kWavesPerBlock + wid;
+#else
     const uint64_t w = (uint64_t)blockIdx.x * kWavesPerBlock + wid;
+#endif
     const uint32_t j = (uint32_t)lane >> rl, i = (uint32_t)lane & (RUN - 1);
     const uint64_t r = (uint64_t)j * Wt + w;   // this lane's run
     const uint64_t p = (r << rl) + i;          // this lane's datagram
@@ -270,13 +276,27 @@ __global__ __launch_bounds__(kGroup* kWavesPerBlock, HY_WAVE_MIN_WAVES) void sal
     }
     uint32_t W = live ? out_width<OBF>(L, B.pkt_cap) : 0u;
     uint64_t ooff, rfirst;   // output offset of the datagram / of its run's first datagram
-    if (PACKED) {   // (RUN = 64) tile prefix + widths of the tile's earlier datagrams + wave scan
+    if (PACKED && RUN == kGroup) {   // tile prefix + widths of the tile's earlier datagrams + wave scan
         const uint64_t p0 = w * kGroup;
         const uint64_t tb = p0 / kTile * kTile;
         uint32_t pre = 0;
         for (uint64_t q = tb + lane; q < p0; q += kGroup) pre += out_width<OBF>(pkt_len(B, q), B.pkt_cap);
         rfirst = uni64(B.tile_prefix[p0 / kTile] + wave_sum(pre));
         ooff = rfirst + wave_incl_scan(W, lane) - W;
+    } else if (PACKED) {   // shorter runs: the same per run, over the run's RUN lanes
+        const uint64_t s0 = r << rl;   // the run's first datagram
+        const uint64_t tb = s0 / kTile * kTile;
+        uint64_t pre = 0;
+        if (s0 < B.n)
+            for (uint64_t q = tb + i; q < s0; q += RUN) pre += out_width<OBF>(pkt_len(B, q), B.pkt_cap);
+        uint64_t inc = W;   // run sum of `pre`, segmented inclusive scan of W inside the run
+        for (uint32_t m = 1; m < RUN; m <<= 1) {
+            pre += __shfl_xor(pre, (int)m, 64);
+            const uint64_t y = __shfl_up(inc, m, 64);
+            if (i >= m) inc += y;
+        }
+        rfirst = s0 < B.n ? B.tile_prefix[s0 / kTile] + pre : 0;
+        ooff = rfirst + inc - W;
     } else {
         ooff = p * B.out_stride;
         rfirst = (r << rl) * B.out_stride;
@@ -481,6 +501,18 @@ __global__ __launch_bounds__(kGroup* kWavesPerBlock, HY_WAVE_MIN_WAVES) void sal
 // sweep a ~80 MB window in address order (whole 64-datagram groups leave a
 // ~630 MB window, tools/region_copy.hip), large enough that few 128-byte
 // lines are shared between runs of different waves.
+#ifndef HY_PACKED_RUN_LOG2
+#define HY_PACKED_RUN_LOG2 6
+#endif
+inline uint32_t wave_packed_run_log2() {   // packed layout: datagrams per run (HYOBFS_PACKED_RUN_LOG2)
+    static int v = -1;
+    if (v < 0) {
+        const char* e = std::getenv("HYOBFS_PACKED_RUN_LOG2");
+        v = e ? std::atoi(e) : HY_PACKED_RUN_LOG2;
+        v = v < 0 ? 0 : v > 6 ? 6 : v;
+    }
+    return (uint32_t)v;
+}
 inline uint32_t wave_run_log2() {
     static int v = -1;
     if (v < 0) {
@@ -496,7 +528,7 @@ void launch_wave_sw(const BatchParams& bp, const KeyParams& k, hipStream_t s) {
     const uint64_t ngroups = div_up(bp.n, kGroup);
     const uint64_t blocks = div_up(ngroups, kWavesPerBlock);
     BatchParams b = bp;
-    b.run_log2 = PACKED ? 6u : wave_run_log2();
+    b.run_log2 = PACKED ? wave_packed_run_log2() : wave_run_log2();
     hipLaunchKernelGGL((salamander_wave_kernel<OBF, PACKED, SW>), dim3((uint32_t)blocks),
                        dim3(kGroup * kWavesPerBlock), 0, s, b, k);
 }

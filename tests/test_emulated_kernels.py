@@ -80,6 +80,14 @@ def test_emulated_wave_kernel_run_lengths(emu_lib, which, args, run_log2):
     _run(emu_lib, which, args, {"HYOBFS_RUN_LOG2": run_log2, "HYOBFS_KERNEL": "wave"})
 
 
+@pytest.mark.parametrize("which,args,run_log2", RUN_CASES + [("bimodal", "3000 1", "3"), ("bimodal", "5000 0", "2")])
+def test_emulated_wave_kernel_packed_run_lengths(emu_lib, which, args, run_log2):
+    """Packed layouts with runs shorter than the 64-datagram group: each run's output
+    base is the tile prefix plus the widths of the tile's earlier datagrams."""
+    _run(emu_lib, which, args, {"HYOBFS_PACKED_RUN_LOG2": run_log2, "HYOBFS_RUN_LOG2": run_log2,
+                                "HYOBFS_KERNEL": "wave"})
+
+
 @pytest.mark.parametrize("which,args,cus", CASES)
 def test_emulated_persistent_kernel(emu_lib, which, args, cus):
     """The persistent workgroup kernel (HYOBFS_KERNEL=persistent) on the same cases."""
