@@ -138,12 +138,63 @@ __global__ __launch_bounds__(256) HY_GK_ATTR void gecko_encode_kernel(KeyParams 
             for (uint32_t j = p; j < plain; ++j) po[j] = (uint8_t)(v >> (8 * (j - p)));
         }
     };
+    // ---- edge windows of frame `lane`: header window, the window holding the
+    // padding/chunk seam and the next one (short chunks), and the last window
+    const uint32_t ehpl = nwin ? G.hp_plain[lane] : 0u, ehp = ehpl & 0xffff, eplain = ehpl >> 16;
+    auto cand = [&](uint32_t c) { return c == 0 ? 0u : c == 3 ? nwin - 1 : (ehp >> 4) + c - 1; };
+    uint32_t emask = 0;   // candidates that are edge windows (not interior, not repeated)
+    if (nwin) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            bool dup = cand(c) >= nwin;
+#pragma unroll
+            for (int d = 0; d < c; ++d) dup = dup || cand(d) == cand(c);
+            if (!dup && !interior(16 * cand(c), ehp, eplain)) emask |= 1u << c;
+        }
+    }
+    auto edge = [&](uint32_t wi) {
+        const uint32_t k = lane, hp = ehp, plain = eplain;
+        const uint8_t* __restrict__ chunk = B.msg + G.chunk_off[k];
+        const uint32_t p = 16 * wi;
+        const uint32_t e = min(p + 16, plain);
+        gk_u128 v = 0;
+        if (p == 0) v = (gk_u128)G.hdr[k] & gk_mask(0, min(e, (uint32_t)HYOBFS_GECKO_HEADER_LEN));
+        const uint32_t plo = max(p, (uint32_t)HYOBFS_GECKO_HEADER_LEN), phi = min(e, hp);
+        if (plo < phi) v |= pad16(k, p) & gk_mask(plo - p, phi - p);
+        const uint32_t clo = max(p, hp);
+        if (clo < e) {   // chunk bytes
+            const uint32_t clen = plain - hp;
+            gk_u128 X = 0;
+            if (p >= hp && p + 16 <= plain) {
+                X = gk_load16u(chunk + (p - hp));
+            } else if (clen >= 16) {   // first or last window of the chunk: one in-bounds load, shifted
+                X = p < hp ? gk_load16u(chunk) << (8 * (hp - p)) : gk_load16u(chunk + (clen - 16)) >> (8 * (p + 16 - plain));
+            } else {
+                for (uint32_t j = clo; j < e; ++j) X |= (gk_u128)chunk[j - hp] << (8 * (j - p));
+            }
+            v |= X & gk_mask(clo - p, e - p);
+        }
+        store(k, p, plain, v ^ G.key[2 * k + (wi & 1)]);
+    };
+    auto edges = [&](uint32_t m) {   // one copy of the edge code (registers: 5 waves/SIMD)
+#pragma unroll 1
+        while (m) {
+            const uint32_t c = __builtin_ctz(m);
+            m &= m - 1;
+            edge(cand(c));
+        }
+    };
     // ---- 2. sweep: window t belongs to the last frame whose first window is <= t.
     // A lane's windows only move forward (t0 + 64 u), so its frame index q does too:
     // it steps over the frames started since its previous window (one or two LDS
-    // reads for frames of >= 32 windows) instead of a fresh 6-step search.
+    // reads for frames of >= 32 windows) instead of a fresh 6-step search.  Edge
+    // windows come after the sweep: storing each inside the iteration whose range
+    // holds it (HY_GK_EDGES_INLINE, meant to let lines split between a frame's
+    // interior and its edges leave the L2 whole) made the sweep divergent, 0.616 ->
+    // 0.826 ms (profiles/r01_ab_gecko/).
     uint32_t q = 0;
-    for (uint32_t t0 = lane; t0 < tw; t0 += 64 * kGkU) {
+    for (uint32_t T = 0; T < tw; T += 64 * kGkU) {
+        const uint32_t t0 = T + lane;
         gk_u128 v[kGkU];
         uint32_t kk[kGkU], pp[kGkU];
         bool ok[kGkU];
@@ -174,43 +225,20 @@ __global__ __launch_bounds__(256) HY_GK_ATTR void gecko_encode_kernel(KeyParams 
 #pragma unroll
         for (int u = 0; u < kGkU; ++u)
             if (ok[u]) store(kk[u], pp[u], 0xFFFFFFFFu, v[u]);
-    }
-    // ---- 3. edge windows of frame `lane`: header window, the window holding the
-    // padding/chunk seam and the next one (short chunks), and the last window
-    if (nwin) {
-        const uint32_t k = lane;
-        const uint32_t hpl = G.hp_plain[k], hp = hpl & 0xffff, plain = hpl >> 16;
-        const uint8_t* __restrict__ chunk = B.msg + G.chunk_off[k];
-        const uint32_t cand[4] = {0u, hp >> 4, (hp >> 4) + 1, nwin - 1};
+#ifdef HY_GK_EDGES_INLINE   // A/B builds only: edges stored inside the sweep iteration
+        if (emask) {
+            const uint32_t ws = G.wstart[lane];
+            uint32_t m = 0;
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            const uint32_t wi = cand[c];
-            bool dup = wi >= nwin;
-#pragma unroll
-            for (int d = 0; d < c; ++d) dup = dup || cand[d] == wi;
-            const uint32_t p = 16 * wi;
-            if (dup || interior(p, hp, plain)) continue;
-            const uint32_t e = min(p + 16, plain);
-            gk_u128 v = 0;
-            if (p == 0) v = (gk_u128)G.hdr[k] & gk_mask(0, min(e, (uint32_t)HYOBFS_GECKO_HEADER_LEN));
-            const uint32_t plo = max(p, (uint32_t)HYOBFS_GECKO_HEADER_LEN), phi = min(e, hp);
-            if (plo < phi) v |= pad16(k, p) & gk_mask(plo - p, phi - p);
-            const uint32_t clo = max(p, hp);
-            if (clo < e) {   // chunk bytes
-                const uint32_t clen = plain - hp;
-                gk_u128 X = 0;
-                if (p >= hp && p + 16 <= plain) {
-                    X = gk_load16u(chunk + (p - hp));
-                } else if (clen >= 16) {   // first or last window of the chunk: one in-bounds load, shifted
-                    X = p < hp ? gk_load16u(chunk) << (8 * (hp - p)) : gk_load16u(chunk + (clen - 16)) >> (8 * (p + 16 - plain));
-                } else {
-                    for (uint32_t j = clo; j < e; ++j) X |= (gk_u128)chunk[j - hp] << (8 * (j - p));
-                }
-                v |= X & gk_mask(clo - p, e - p);
-            }
-            store(k, p, plain, v ^ G.key[2 * k + (wi & 1)]);
+            for (int c = 0; c < 4; ++c)
+                if ((emask >> c & 1) && ws + cand(c) - T < 64u * kGkU) m |= 1u << c;
+            edges(m);
         }
+#endif
     }
+#ifndef HY_GK_EDGES_INLINE   // ---- 3. all edge windows after the sweep
+    edges(emask);
+#endif
 }
 
 __global__ __launch_bounds__(256) void gecko_parse_kernel(const uint8_t* in, const uint64_t* in_off,
