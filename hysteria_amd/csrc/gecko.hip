@@ -283,7 +283,11 @@ hipError_t launch_gecko_encode(const KeyParams& k, const hyobfs_gecko_batch& b, 
 #endif
     // (Instantiating per salt word as the wave kernel does cuts 96 -> 60 VGPRs, 5 -> 8
     // waves/SIMD, and measured 4 % slower: profiles/r01_ab_gecko/.)
-    hipLaunchKernelGGL(gecko_encode_kernel, dim3((uint32_t)((b.n + 255) / 256)), dim3(256), 0, s, k, b);
+    static const uint32_t lds_pad = [] {   // A/B only: unused dynamic LDS to cap workgroups per CU
+        const char* e = std::getenv("HYOBFS_GK_LDS_PAD");
+        return e ? (uint32_t)std::atoi(e) : 0u;
+    }();
+    hipLaunchKernelGGL(gecko_encode_kernel, dim3((uint32_t)((b.n + 255) / 256)), dim3(256), lds_pad, s, k, b);
     return hipGetLastError();
 }
 
