@@ -6,24 +6,33 @@ Metric (BASELINE.json): "device-resident packet-obfs GiB/s @ 1200B datagrams,
 datagram) over the whole synthetic batch, inputs already resident in HBM.
 
   * N = 1: BASELINE.json configs[1] -- 1,048,576 x 1200 B datagrams, one batch.
-  * N > 1: one process per GPU (torch.distributed.run); rank r owns packets
-    [r*P, (r+1)*P) of the global synthetic batch (weak scaling, P per GPU,
-    no collective on the data path; gloo only for the timing barrier/max).
+    The line also carries a `bimodal` object: configs[2], 4M datagrams of the
+    40 % 64 B / 60 % 1350 B mix, packed output.
+  * N > 1: BASELINE.json configs[3] -- 8,388,608 x 1200 B datagrams per GPU
+    (64M over 8 GPUs), one process per GPU; rank r owns datagrams
+    [r*P, (r+1)*P) of the global synthetic batch (weak scaling, no collective
+    on the data path; gloo only for the timing barrier and the max).
+    `python bench.py --gpus N` starts the N rank processes itself (this process
+    never touches the GPU); under torch.distributed.run it is one rank.
 
 value = sum over ranks of plaintext payload bytes / max-over-ranks wall time
 of the K timed steps / 2^30 (Go's b.SetBytes numerator).  The roofline is for
 the obfuscate kernel: 2L+16 algorithmic HBM bytes per datagram / its average
-launch time from HIP events on the launch stream.  cpu_baseline times the C
-restatement in oracle/ (a port: no Go toolchain exists on the box) on host
-cores.  --workload bimodal runs BASELINE configs[2] (ragged, packed output).
+launch time from HIP events on the launch stream.  `traffic` is the PMC
+figure from profiles/pmc_traffic.json, used only when its entry was measured
+on the same kernel sources (sha256 of hysteria_amd/csrc/*, see
+scripts/collect_profiles.sh).  cpu_baseline times the C restatement in oracle/
+(a port: no Go toolchain exists on the box) on host cores.
 """
 from __future__ import annotations
 
 import argparse
+import glob
 import hashlib
 import json
 import os
 import platform
+import subprocess
 import sys
 import time
 
@@ -32,6 +41,20 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md); 6.29 TB/s measured float4 copy
 PSK = b"average_password"
+METRIC = "device-resident packet-obfs GiB/s @ 1200B datagrams, 1/2/4/8 MI355X"
+# the obfuscate kernel each workload runs, per --kernel (rocprof names in profiles/)
+KERNEL_NAMES = {
+    "uniform": {"auto": "salamander_wave_kernel<obfuscate, slotted> (salamander_wave.h)",
+                "uniform": "salamander_uniform_kernel<obfuscate> (salamander_uniform.h)",
+                "stream": "keys pass + salamander_stream_kernel<obfuscate> (salamander_stream.h)",
+                "wave": "salamander_wave_kernel<obfuscate, slotted> (salamander_wave.h)",
+                "persistent": "salamander_kernel<obfuscate, slotted> (salamander_device.h)"},
+    "bimodal": {"auto": "salamander_kernel<obfuscate, packed> (salamander_device.h) + tile-sum scan",
+                "uniform": "salamander_kernel<obfuscate, packed> (salamander_device.h) + tile-sum scan",
+                "stream": "salamander_kernel<obfuscate, packed> (salamander_device.h) + tile-sum scan",
+                "wave": "salamander_wave_kernel<obfuscate, packed> (salamander_wave.h) + tile-sum scan",
+                "persistent": "salamander_kernel<obfuscate, packed> (salamander_device.h) + tile-sum scan"},
+}
 
 
 def parse():
@@ -45,7 +68,33 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="bounded CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
+    ap.add_argument("--no-bimodal", action="store_true", help="N=1: skip the configs[2] sub-object")
+    ap.add_argument("--kernel", choices=["auto", "wave", "persistent", "uniform", "stream"], default="auto")
     return ap.parse_args()
+
+
+def kernel_src_sha() -> str:
+    """sha256 over the kernel sources: keys the committed PMC traffic figures."""
+    h = hashlib.sha256()
+    for p in sorted(glob.glob(os.path.join(ROOT, "hysteria_amd", "csrc", "*"))):
+        if os.path.isfile(p) and p.endswith((".h", ".hip", ".cpp", "Makefile")):
+            h.update(os.path.basename(p).encode())
+            h.update(open(p, "rb").read())
+    return h.hexdigest()[:16]
+
+
+def pmc_traffic(workload: str, direction: str, datagrams: int, length) -> dict | None:
+    f = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        entries = json.load(open(f)).get("entries", [])
+    except (OSError, ValueError, AttributeError):
+        return None
+    sha = kernel_src_sha()
+    for e in entries:
+        if (e.get("src_sha") == sha and e.get("workload") == workload and e.get("direction") == direction
+                and e.get("datagrams") == datagrams and e.get("len") == length):
+            return e
+    return None
 
 
 def cpu_model() -> str:
@@ -99,11 +148,103 @@ def cpu_baseline(L: int, seconds: float) -> dict:
             "go_reference": "unavailable: no Go toolchain on the box"}
 
 
+def spawn_ranks(args) -> int:
+    """--gpus N without an external launcher: one child process per rank (this
+    parent never initialises HIP), rank 0 prints the line.  If a rank fails the
+    others are stopped (by their own PIDs) and its exit code is returned."""
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                   LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc, pending = 0, set(range(len(procs)))
+    while pending:
+        for i in sorted(pending):
+            r = procs[i].poll()
+            if r is None:
+                continue
+            pending.discard(i)
+            if r != 0 and rc == 0:
+                rc = r
+                for j in pending:
+                    procs[j].kill()
+        time.sleep(0.1)
+    return rc
+
+
+# ------------------------------------------------------------------ workloads
+def setup_uniform(hy, obfs, dev, P, L, first):
+    import torch
+    inp = torch.empty(P * L, dtype=torch.uint8, device=dev)
+    hy.synth_stream(inp, P * L, 1, first * L)
+    salts = torch.empty(P, dtype=torch.int64, device=dev)
+    hy.synth_u64(salts, P, 2, first)
+    wire = torch.empty(P * (L + 8), dtype=torch.uint8, device=dev)
+    back = torch.empty(P * L, dtype=torch.uint8, device=dev)
+
+    def step_obf():
+        obfs.obfuscate_batch(inp, P, in_stride=L, len_uniform=L, salts=salts, out=wire, out_stride=L + 8)
+
+    def step_deobf():
+        obfs.deobfuscate_batch(wire, P, in_stride=L + 8, len_uniform=L + 8, out=back, out_stride=L)
+
+    return dict(obf=step_obf, deobf=step_deobf, payload=P * L, obf_bytes=P * (2 * L + 16),
+                deobf_bytes=P * (2 * L + 8), inp=inp, wire=wire, back=back, n=P, len=L)
+
+
+def setup_bimodal(hy, obfs, dev, P, first):
+    import torch
+    lens = torch.empty(P, dtype=torch.int32, device=dev)
+    hy.synth_bimodal_lengths(lens, P, 3, first)
+    in_off = torch.zeros(P, dtype=torch.int64, device=dev)
+    in_off[1:] = torch.cumsum(lens[:-1].to(torch.int64), 0)
+    total_in = int(lens.to(torch.int64).sum())
+    inp = torch.empty(total_in + 16, dtype=torch.uint8, device=dev)
+    # stream offset of this rank's shard (global packed input): the lengths of
+    # every earlier datagram, generated on device in chunks
+    start = 0
+    if first:
+        tmp = torch.empty(min(first, 1 << 24), dtype=torch.int32, device=dev)
+        done = 0
+        while done < first:
+            k = min(first - done, tmp.numel())
+            hy.synth_bimodal_lengths(tmp, k, 3, done)
+            start += int(tmp[:k].to(torch.int64).sum())
+            done += k
+    hy.synth_stream(inp, total_in, 1, start)
+    salts = torch.empty(P, dtype=torch.int64, device=dev)
+    hy.synth_u64(salts, P, 2, first)
+    cap = total_in + 8 * P
+    wire = torch.empty(cap, dtype=torch.uint8, device=dev)
+    out_off = torch.empty(P, dtype=torch.int64, device=dev)
+    out_len = torch.empty(P, dtype=torch.int32, device=dev)
+    back = torch.empty(total_in + 16, dtype=torch.uint8, device=dev)
+    ws = torch.empty(hy.workspace_size(P), dtype=torch.uint8, device=dev)
+
+    def step_obf():
+        obfs.obfuscate_batch(inp, P, in_off=in_off, in_len=lens, salts=salts, out=wire, out_cap=cap,
+                             out_off=out_off, out_len=out_len, workspace=ws, workspace_bytes=ws.numel())
+
+    def step_deobf():
+        obfs.deobfuscate_batch(wire, P, in_off=out_off, in_len=out_len, out=back, out_cap=total_in,
+                               workspace=ws, workspace_bytes=ws.numel())
+
+    return dict(obf=step_obf, deobf=step_deobf, payload=total_in, obf_bytes=2 * total_in + 16 * P,
+                deobf_bytes=2 * total_in + 8 * P, inp=inp, wire=wire, back=back, n=P, len="bimodal")
+
+
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args))
+
     import torch
     import torch.distributed as dist
-    import hysteria_amd
+    import hysteria_amd as hy
     from hysteria_amd.shard import weak_shard
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -127,78 +268,17 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t[0])
 
-    obfs = hysteria_amd.SalamanderObfuscator(PSK, local)
+    def allgather(x: float) -> list:
+        if world == 1:
+            return [x]
+        out = [torch.zeros(1, dtype=torch.float64) for _ in range(world)]
+        dist.all_gather(out, torch.tensor([x], dtype=torch.float64))
+        return [float(t[0]) for t in out]
+
+    obfs = hy.SalamanderObfuscator(PSK, local)
+    obfs.set_kernel(args.kernel)
     stream = torch.cuda.current_stream(dev)
     L = args.len
-
-    if args.workload == "uniform":
-        P = args.packets_per_gpu or (1 << 20)
-        first, P = weak_shard(P, rank)
-        inp = torch.empty(P * L, dtype=torch.uint8, device=dev)
-        hysteria_amd.synth_stream(inp, P * L, 1, first * L)
-        salts = torch.empty(P, dtype=torch.int64, device=dev)
-        hysteria_amd.synth_u64(salts, P, 2, first)
-        wire = torch.empty(P * (L + 8), dtype=torch.uint8, device=dev)
-        back = torch.empty(P * L, dtype=torch.uint8, device=dev)
-        payload_bytes = P * L
-        obf_bytes = P * (2 * L + 16)      # algorithmic HBM bytes / launch
-        deobf_bytes = P * (2 * L + 8)
-
-        def step_obf():
-            obfs.obfuscate_batch(inp, P, in_stride=L, len_uniform=L, salts=salts, out=wire,
-                                 out_stride=L + 8)
-
-        def step_deobf():
-            obfs.deobfuscate_batch(wire, P, in_stride=L + 8, len_uniform=L + 8, out=back, out_stride=L)
-        config = {"workload": f"uniform {P} x {L} B datagrams per GPU, slotted (= packed) output",
-                  "datagrams_per_gpu": P, "datagram_len": L, "global_datagrams": P * world,
-                  "psk": PSK.decode(), "parallelism": f"packet-index shards x{world}"}
-    else:
-        P = args.packets_per_gpu or (1 << 22)
-        first, P = weak_shard(P, rank)
-        lens = torch.empty(P, dtype=torch.int32, device=dev)
-        hysteria_amd.synth_bimodal_lengths(lens, P, 3, first)
-        in_off = torch.zeros(P, dtype=torch.int64, device=dev)
-        in_off[1:] = torch.cumsum(lens[:-1].to(torch.int64), 0)
-        total_in = int(lens.to(torch.int64).sum())
-        inp = torch.empty(total_in + 16, dtype=torch.uint8, device=dev)
-        # stream offset of this rank's shard (global packed input): computed from the lengths
-        # of every earlier packet, generated on device in chunks
-        start = 0
-        if first:
-            tmp = torch.empty(min(first, 1 << 24), dtype=torch.int32, device=dev)
-            done = 0
-            while done < first:
-                k = min(first - done, tmp.numel())
-                hysteria_amd.synth_bimodal_lengths(tmp, k, 3, done)
-                start += int(tmp[:k].to(torch.int64).sum())
-                done += k
-        hysteria_amd.synth_stream(inp, total_in, 1, start)
-        salts = torch.empty(P, dtype=torch.int64, device=dev)
-        hysteria_amd.synth_u64(salts, P, 2, first)
-        cap = total_in + 8 * P
-        wire = torch.empty(cap, dtype=torch.uint8, device=dev)
-        out_off = torch.empty(P, dtype=torch.int64, device=dev)
-        out_len = torch.empty(P, dtype=torch.int32, device=dev)
-        back = torch.empty(total_in + 16, dtype=torch.uint8, device=dev)
-        ws = torch.empty(hysteria_amd.workspace_size(P), dtype=torch.uint8, device=dev)
-        payload_bytes = total_in
-        obf_bytes = 2 * total_in + 16 * P
-        deobf_bytes = 2 * total_in + 8 * P
-
-        def step_obf():
-            obfs.obfuscate_batch(inp, P, in_off=in_off, in_len=lens, salts=salts, out=wire, out_cap=cap,
-                                 out_off=out_off, out_len=out_len, workspace=ws,
-                                 workspace_bytes=ws.numel())
-
-        def step_deobf():
-            obfs.deobfuscate_batch(wire, P, in_off=out_off, in_len=out_len, out=back, out_cap=total_in,
-                                   workspace=ws, workspace_bytes=ws.numel())
-        config = {"workload": f"bimodal 40% 64 B / 60% 1350 B, {P} datagrams per GPU, packed output",
-                  "datagrams_per_gpu": P, "global_datagrams": P * world, "psk": PSK.decode(),
-                  "parallelism": f"packet-index shards x{world}"}
-
-    torch.cuda.synchronize()
 
     def timed(fn, steps, warmup):
         for _ in range(warmup):
@@ -213,62 +293,99 @@ def main():
         ev1.record(stream)
         torch.cuda.synchronize()
         barrier()
-        wall = time.perf_counter() - t0
-        return allmax(wall), ev0.elapsed_time(ev1) / 1e3 / steps
+        mine = time.perf_counter() - t0
+        return allmax(mine), mine, ev0.elapsed_time(ev1) / 1e3 / steps
 
-    wall_obf, ev_obf = timed(step_obf, args.steps, args.warmup)
-    wall_deobf, ev_deobf = timed(step_deobf, args.steps, args.warmup)
+    def measure(w, workload):
+        """Timed obfuscate and deobfuscate passes of one workload: the line's fields."""
+        wall_obf, mine_obf, ev_obf = timed(w["obf"], args.steps, args.warmup)
+        wall_deobf, _, ev_deobf = timed(w["deobf"], args.steps, args.warmup)
+        total_payload = w["payload"] * world * args.steps   # every step processes the whole batch
+        achieved = w["obf_bytes"] / ev_obf / 1e9
+        roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None, "kernel": KERNEL_NAMES[workload][args.kernel],
+                "algorithmic_bytes_per_launch": w["obf_bytes"], "avg_launch_ms": round(ev_obf * 1e3, 4),
+                "kernel_src_sha": kernel_src_sha()}
+        t = pmc_traffic(workload, "obfuscate", w["n"], w["len"])
+        if t:
+            roof["traffic"] = t["hbm_bytes_per_launch"]
+            roof["traffic_over_algorithmic"] = round(t["hbm_bytes_per_launch"] / w["obf_bytes"], 4)
+            roof["traffic_source"] = t.get("source")
+        deob = {"value": round(total_payload / wall_deobf / 2**30, 2), "unit": "GiB/s",
+                "ms_per_step": round(wall_deobf / args.steps * 1e3, 4),
+                "achieved_GBs": round(w["deobf_bytes"] / ev_deobf / 1e9, 1),
+                "frac": round(w["deobf_bytes"] / ev_deobf / 1e9 / HBM_PEAK_GBS, 4),
+                "avg_launch_ms": round(ev_deobf * 1e3, 4), "algorithmic_bytes_per_launch": w["deobf_bytes"]}
+        t = pmc_traffic(workload, "deobfuscate", w["n"], w["len"])
+        if t:
+            deob["traffic"] = t["hbm_bytes_per_launch"]
+            deob["traffic_over_algorithmic"] = round(t["hbm_bytes_per_launch"] / w["deobf_bytes"], 4)
+        per_gpu = [round(w["payload"] * args.steps / x / 2**30, 2) for x in allgather(mine_obf)]
+        return dict(value=total_payload / wall_obf / 2**30, ms=wall_obf / args.steps * 1e3, roofline=roof,
+                    deobfuscate=deob, per_gpu=per_gpu)
+
+    if args.workload == "uniform":
+        P = args.packets_per_gpu or ((1 << 20) if world == 1 else (1 << 23))
+        first, P = weak_shard(P, rank)
+        w = setup_uniform(hy, obfs, dev, P, L, first)
+        cfg_name = "configs[1]" if world == 1 else "configs[3] shard"
+        config = {"workload": f"uniform {P} x {L} B datagrams per GPU ({cfg_name}), dense slotted output",
+                  "datagrams_per_gpu": P, "datagram_len": L, "global_datagrams": P * world,
+                  "psk": PSK.decode(), "parallelism": f"packet-index shards x{world}"}
+    else:
+        P = args.packets_per_gpu or (1 << 22)
+        first, P = weak_shard(P, rank)
+        w = setup_bimodal(hy, obfs, dev, P, first)
+        config = {"workload": f"bimodal 40% 64 B / 60% 1350 B, {P} datagrams per GPU, packed output",
+                  "datagrams_per_gpu": P, "global_datagrams": P * world, "psk": PSK.decode(),
+                  "parallelism": f"packet-index shards x{world}"}
+    torch.cuda.synchronize()
+    m = measure(w, args.workload)
 
     parity = None
-    if rank == 0 and not args.no_parity and args.workload == "uniform" and P == (1 << 20) and L == 1200:
-        with open(os.path.join(ROOT, "tests", "golden", "batch_digests.json")) as f:
-            want = json.load(f)["config2_1M_x_1200"]["obf_sha256"]
+    if rank == 0 and not args.no_parity:
         torch.cuda.synchronize()
-        got = hashlib.sha256(wire.cpu().numpy().tobytes()).hexdigest()
-        rt = bool(torch.equal(back, inp))
-        parity = {"sha256_match_config2": got == want, "roundtrip_identity": rt}
-    elif rank == 0 and not args.no_parity:
-        torch.cuda.synchronize()
-        parity = {"roundtrip_identity": bool(torch.equal(back[:payload_bytes], inp[:payload_bytes]))}
+        parity = {"roundtrip_identity": bool(torch.equal(w["back"][:w["payload"]], w["inp"][:w["payload"]]))}
+        if args.workload == "uniform" and P == (1 << 20) and L == 1200 and first == 0:
+            with open(os.path.join(ROOT, "tests", "golden", "batch_digests.json")) as f:
+                want = json.load(f)["config2_1M_x_1200"]["obf_sha256"]
+            parity["sha256_match_config2"] = hashlib.sha256(w["wire"].cpu().numpy().tobytes()).hexdigest() == want
+    del w
 
-    # wall_* cover all K timed steps: every step processes the whole batch once
-    total_payload = payload_bytes * world * args.steps
-    value = total_payload / wall_obf / 2**30
-    achieved = obf_bytes / ev_obf / 1e9
     res = {
-        "metric": "device-resident packet-obfs GiB/s @ 1200B datagrams, 1/2/4/8 MI355X",
-        "value": round(value, 2),
+        "metric": METRIC,
+        "value": round(m["value"], 2),
         "unit": "GiB/s",
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": round(wall_obf / args.steps * 1e3, 4),
+        "ms_per_step": round(m["ms"], 4),
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u8",
         "data": "synthetic (SplitMix64 seeds 1/2/3, generated on device; PSK average_password)",
         "config": config,
-        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                     "kernel": ("salamander_wave_kernel<obfuscate, slotted>" if args.workload == "uniform"
-                                else "salamander_kernel<obfuscate, packed> (+ tile-sum scan)"),
-                     "algorithmic_bytes_per_launch": obf_bytes, "avg_launch_ms": round(ev_obf * 1e3, 4)},
-        "deobfuscate": {"value": round(total_payload / wall_deobf / 2**30, 2), "unit": "GiB/s",
-                        "ms_per_step": round(wall_deobf / args.steps * 1e3, 4),
-                        "achieved_GBs": round(deobf_bytes / ev_deobf / 1e9, 1),
-                        "frac": round(deobf_bytes / ev_deobf / 1e9 / HBM_PEAK_GBS, 4)},
+        "roofline": m["roofline"],
+        "per_gpu_GiBs": m["per_gpu"],
+        "deobfuscate": m["deobfuscate"],
         "parity": parity,
     }
-    traffic_file = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if os.path.exists(traffic_file) and args.workload == "uniform":
-        try:
-            tj = json.load(open(traffic_file))
-            if tj.get("datagrams") == P and tj.get("len") == L:
-                res["roofline"]["traffic"] = tj["hbm_bytes_per_launch"]
-                res["roofline"]["traffic_source"] = tj.get("source", traffic_file)
-        except (ValueError, KeyError):
-            pass
+
+    # configs[2] beside the headline (N = 1 only): the ragged mix with packed output
+    if world == 1 and args.workload == "uniform" and not args.no_bimodal:
+        torch.cuda.empty_cache()
+        wb = setup_bimodal(hy, obfs, dev, 1 << 22, 0)
+        torch.cuda.synchronize()
+        mb = measure(wb, "bimodal")
+        torch.cuda.synchronize()
+        rt = bool(torch.equal(wb["back"][:wb["payload"]], wb["inp"][:wb["payload"]]))
+        res["bimodal"] = {"workload": "configs[2]: 4194304 datagrams, 40% 64 B / 60% 1350 B, packed output",
+                          "value": round(mb["value"], 2), "unit": "GiB/s", "ms_per_step": round(mb["ms"], 4),
+                          "roofline": mb["roofline"], "deobfuscate": mb["deobfuscate"],
+                          "parity": {"roundtrip_identity": rt}}
+        del wb
+
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(1200, args.cpu_seconds)
     elif rank == 0:

@@ -74,9 +74,11 @@ __global__ __launch_bounds__(256) HY_GK_ATTR void gecko_encode_kernel(KeyParams 
     if (f < B.n) {
         const hyobfs_gecko_frame fr = B.frames[f];
         const uint32_t total = fr.idx_total & 0x0f, idx = fr.idx_total >> 4;
-        const uint32_t hp = HYOBFS_GECKO_HEADER_LEN + fr.pad_len, plain = hp + fr.chunk_len;
+        const uint32_t hp = HYOBFS_GECKO_HEADER_LEN + fr.pad_len;
+        const uint64_t plain64 = (uint64_t)hp + fr.chunk_len;   // 64-bit: a hostile chunk_len must not wrap
+        const uint32_t plain = (uint32_t)plain64;
         if (total >= HYOBFS_GECKO_MIN_CHUNKS && total <= HYOBFS_GECKO_MAX_CHUNKS && idx < total &&
-            HYOBFS_SALT_LEN + plain <= HYOBFS_GECKO_BUFFER_SIZE) {   // else: skipped, nothing written
+            HYOBFS_SALT_LEN + plain64 <= HYOBFS_GECKO_BUFFER_SIZE) {   // else: skipped, nothing written
             nwin = (plain + 15) >> 4;
             const uint64_t oo = B.out_off[f];
             G.out_off[lane] = oo;

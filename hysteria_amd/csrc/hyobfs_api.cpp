@@ -38,9 +38,17 @@ struct hyobfs_salamander {
     uint8_t* stage = nullptr;
     uint8_t* stage_dev = nullptr;
     size_t stage_cap = 0;       // bytes for each of in and out
-    // context-owned batch workspace
-    void* ws = nullptr;
-    uint64_t ws_cap = 0;
+    // context-owned packed-batch scratch, one buffer per stream (a buffer is only
+    // ever used by launches on its own stream, so stream order protects it).
+    // ws_mu is held from the lookup through the kernel launch, so a growing call
+    // can synchronise that stream and free the old buffer safely.
+    struct StreamWs {
+        hipStream_t s = nullptr;
+        void* p = nullptr;
+        uint64_t cap = 0;
+    };
+    std::vector<StreamWs> ws;
+    std::mutex ws_mu;
     // host-batch pipeline: three slots, one stream each (see *_host)
     struct Slot {
         hipStream_t s = nullptr;
@@ -226,6 +234,30 @@ size_t run_one(hyobfs_salamander* c, bool obf, const uint8_t* in, size_t in_len,
     return W;
 }
 
+// The context's scratch for stream s, grown to `need` bytes.  Caller holds c->ws_mu.
+void* stream_workspace(hyobfs_salamander* c, hipStream_t s, uint64_t need) {
+    hyobfs_salamander::StreamWs* e = nullptr;
+    for (auto& x : c->ws)
+        if (x.s == s) e = &x;
+    if (!e) {
+        c->ws.push_back({s, nullptr, 0});
+        e = &c->ws.back();
+    }
+    if (e->cap < need) {
+        if (e->p) {
+            // only launches on s use this buffer, and every one of them was
+            // enqueued under ws_mu: once s drains, nothing references it
+            if (hipStreamSynchronize(s) != hipSuccess) return nullptr;
+            (void)hipFree(e->p);
+        }
+        e->p = nullptr;
+        e->cap = 0;
+        if (hipMalloc(&e->p, need) != hipSuccess) return nullptr;
+        e->cap = need;
+    }
+    return e->p;
+}
+
 int validate_and_fill(hyobfs_salamander* c, const hyobfs_batch* b, bool obf, BatchParams& bp,
                       hipStream_t s) {
     if (!c || !b) return HYOBFS_ERR_INVALID;
@@ -253,27 +285,22 @@ int validate_and_fill(hyobfs_salamander* c, const hyobfs_batch* b, bool obf, Bat
     bp.kernel = c->kernel;
     if (b->out_total && hipMemsetAsync(b->out_total, 0, sizeof(uint64_t), s) != hipSuccess)
         return HYOBFS_ERR_HIP;
-    if (b->n && b->out_stride == 0) {   // packed: tile-sum scratch
-        const uint64_t need = hyobfs_batch_workspace_size(b->n);
-        if (b->workspace) {
-            if (b->workspace_bytes < need) return HYOBFS_ERR_INVALID;
-            bp.tile_sums = static_cast<uint64_t*>(b->workspace);
-        } else {
-            std::lock_guard<std::mutex> lk(c->mu);
-            if (c->ws_cap < need) {
-                if (c->ws) {
-                    (void)hipStreamSynchronize(s);
-                    (void)hipFree(c->ws);
-                }
-                c->ws = nullptr;
-                c->ws_cap = 0;
-                if (hipMalloc(&c->ws, need) != hipSuccess) return HYOBFS_ERR_NOMEM;
-                c->ws_cap = need;
-            }
-            bp.tile_sums = static_cast<uint64_t*>(c->ws);
-        }
+    if (b->n && b->out_stride == 0 && b->workspace) {   // packed: caller's tile-sum scratch
+        if (b->workspace_bytes < hyobfs_batch_workspace_size(b->n)) return HYOBFS_ERR_INVALID;
+        bp.tile_sums = static_cast<uint64_t*>(b->workspace);
     }
     return HYOBFS_OK;
+}
+
+// Bytes of the context's per-stream scratch a batch needs: the tile sums of a
+// packed batch without a caller workspace, then (the two-pass stream kernel)
+// 32 bytes of key per datagram.
+inline uint64_t ctx_ws_bytes(const hyobfs_salamander* c, const hyobfs_batch* b, uint64_t& keys_off) {
+    uint64_t need = 0;
+    if (b->n && b->out_stride == 0 && !b->workspace) need = (hyobfs_batch_workspace_size(b->n) + 255) & ~255ull;
+    keys_off = need;
+    if (b->n >= 2 && hyobfs::resolve_kernel(c->kernel) == HYOBFS_KERNEL_STREAM) need += 32 * b->n;
+    return need;
 }
 
 int run_batch(hyobfs_salamander* c, const hyobfs_batch* b, void* stream, bool obf) {
@@ -284,6 +311,15 @@ int run_batch(hyobfs_salamander* c, const hyobfs_batch* b, void* stream, bool ob
     BatchParams bp;
     const int rc = validate_and_fill(c, b, obf, bp, s);
     if (rc != HYOBFS_OK) return rc;
+    std::unique_lock<std::mutex> ws_lk(c->ws_mu, std::defer_lock);
+    uint64_t keys_off = 0;
+    if (const uint64_t need = ctx_ws_bytes(c, b, keys_off)) {   // held through the launch (see StreamWs)
+        ws_lk.lock();
+        auto* w = static_cast<uint8_t*>(stream_workspace(c, s, need));
+        if (!w) return HYOBFS_ERR_NOMEM;
+        if (keys_off) bp.tile_sums = reinterpret_cast<uint64_t*>(w);
+        if (need > keys_off) bp.keys = reinterpret_cast<uint64_t*>(w + keys_off);
+    }
 #ifdef HY_BOUNDS_CHECK
     // debug variant: HYOBFS_DEBUG_IN_BYTES bounds the input; report the first bad access
     static unsigned long long* dbg = nullptr;
@@ -377,7 +413,11 @@ int run_host(hyobfs_salamander* c, const hyobfs_batch* b, uint64_t chunk, bool o
         if (rc != HYOBFS_OK) return HYOBFS_ERR_NOMEM;
     }
     const uint64_t nchunks = (b->n + chunk - 1) / chunk;
-    for (uint64_t k = 0; k < nchunks; ++k) {
+    // enqueue every chunk; on a failure stop enqueueing, but always drain the
+    // three streams before returning: copies already queued still reference
+    // the caller's host buffers
+    auto enqueue = [&]() -> int {
+      for (uint64_t k = 0; k < nchunks; ++k) {
         auto& sl = c->slot[k % 3];
         const uint64_t first = k * chunk, m = std::min<uint64_t>(chunk, b->n - first);
         hipStream_t s = sl.s;
@@ -412,10 +452,13 @@ int run_host(hyobfs_salamander* c, const hyobfs_batch* b, uint64_t chunk, bool o
         if (b->out_len &&
             hipMemcpyAsync(b->out_len + first, sl.olen, m * 4, hipMemcpyDeviceToHost, s) != hipSuccess)
             return HYOBFS_ERR_HIP;
-    }
+      }
+      return HYOBFS_OK;
+    };
+    int rc = enqueue();
     for (auto& sl : c->slot)
-        if (hipStreamSynchronize(sl.s) != hipSuccess) return HYOBFS_ERR_HIP;
-    return HYOBFS_OK;
+        if (hipStreamSynchronize(sl.s) != hipSuccess && rc == HYOBFS_OK) rc = HYOBFS_ERR_HIP;
+    return rc;
 }
 
 }  // namespace
@@ -473,7 +516,9 @@ void hyobfs_salamander_free(hyobfs_salamander* c) {
             (void)hipStreamSynchronize(c->stream);
             (void)hipStreamDestroy(c->stream);
         }
-        if (c->ws) (void)hipFree(c->ws);
+        // the callers' streams may be gone by now: wait for the whole device
+        if (!c->ws.empty()) (void)hipDeviceSynchronize();
+        for (auto& e : c->ws) (void)hipFree(e.p);
         if (c->stage) (void)hipHostFree(c->stage);
         for (auto& sl : c->slot) {
             if (sl.s) {
@@ -494,7 +539,7 @@ void hyobfs_salamander_free(hyobfs_salamander* c) {
 int hyobfs_salamander_device(const hyobfs_salamander* c) { return c ? c->device : -1; }
 
 int hyobfs_salamander_set_kernel(hyobfs_salamander* c, int kernel) {
-    if (!c || kernel < HYOBFS_KERNEL_AUTO || kernel > HYOBFS_KERNEL_PERSISTENT) return HYOBFS_ERR_INVALID;
+    if (!c || kernel < HYOBFS_KERNEL_AUTO || kernel > HYOBFS_KERNEL_STREAM) return HYOBFS_ERR_INVALID;
     c->kernel = kernel;
     return HYOBFS_OK;
 }
@@ -615,14 +660,19 @@ int hyobfs_shard_bounds(const uint32_t* in_len, uint64_t n, int nshards, uint64_
     return HYOBFS_OK;
 }
 
+#ifdef HY_GK_KEYS_KERNEL   // A/B builds only: keys from a separate keys pass
 uint64_t hyobfs_gecko_workspace_size(uint64_t n) { return 32 * n; }
+#else   // the shipped kernel derives keys in registers: no workspace
+uint64_t hyobfs_gecko_workspace_size(uint64_t) { return 0; }
+#endif
 
 int hyobfs_gecko_encode_batch(hyobfs_salamander* c, const hyobfs_gecko_batch* b, void* stream) {
     if (!c || !b) return HYOBFS_ERR_INVALID;
     if (b->n == 0) return HYOBFS_OK;
-    if (!b->msg || !b->frames || !b->salts || !b->out || !b->out_off || !b->workspace ||
-        b->workspace_bytes < hyobfs_gecko_workspace_size(b->n))
+    if (!b->msg || !b->frames || !b->salts || !b->out || !b->out_off)
         return HYOBFS_ERR_INVALID;
+    const uint64_t ws_need = hyobfs_gecko_workspace_size(b->n);
+    if (ws_need && (!b->workspace || b->workspace_bytes < ws_need)) return HYOBFS_ERR_INVALID;
     DeviceGuard g(c->device);
     if (!g.ok) return HYOBFS_ERR_HIP;
     return hyobfs::launch_gecko_encode(c->kp, *b, static_cast<hipStream_t>(stream)) == hipSuccess ? HYOBFS_OK

@@ -163,9 +163,11 @@ int hyobfs_conn_read_batch(hyobfs_conn* c, hyobfs_dgram* msgs, uint32_t n) {
         }
         int got = 0;
         for (int i = 0; i < k; ++i) {
-            const uint32_t m = c->rx.olen[i];
-            if (m == 0 || m > msgs[got].cap) continue;   // Deobfuscate returned 0: dropped
-            memcpy(msgs[got].buf, c->rx.out + (size_t)i * kBuf, m);
+            // an empty datagram is a 0-byte read, as ReadFrom returns it (conn.go:77-80)
+            const bool empty = c->rx.len[i] == 0;
+            const uint32_t m = empty ? 0u : c->rx.olen[i];
+            if (!empty && (m == 0 || m > msgs[got].cap)) continue;   // Deobfuscate returned 0: dropped
+            if (m) memcpy(msgs[got].buf, c->rx.out + (size_t)i * kBuf, m);
             msgs[got].len = m;
             const uint32_t al = std::min<uint32_t>(c->rmsg[i].msg_hdr.msg_namelen, sizeof msgs[got].addr);
             memcpy(msgs[got].addr, &c->raddr[i], al);

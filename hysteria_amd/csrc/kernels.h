@@ -63,6 +63,7 @@ struct BatchParams {
     unsigned long long* out_total;
     const uint64_t* tile_prefix;  // packed: exclusive prefix of tile sums (ntiles+1)
     uint64_t* tile_sums;          // packed: scratch, ntiles+1 entries
+    uint64_t* keys;               // stream kernel: scratch, 4 key words per datagram (NULL: not available)
     uint64_t part_len;            // main kernel: n / grid datagrams per workgroup ...
     uint64_t part_rem;            // ... plus one for the first n % grid workgroups
     uint32_t run_log2;            // wave kernel: datagrams per run = 2^run_log2
@@ -73,6 +74,9 @@ struct BatchParams {
     uint64_t dbg_in_bytes;
 };
 
+// HYOBFS_KERNEL_* that a context's setting resolves to (AUTO: the
+// HYOBFS_KERNEL environment variable, else 0)
+int resolve_kernel(int ctx_kernel);
 hipError_t launch_salamander(bool obfuscate, const BatchParams& b, const KeyParams& k,
                              hipStream_t s);
 hipError_t launch_keys(const KeyParams& k, const uint64_t* salts, uint8_t* keys, uint64_t n,

@@ -18,7 +18,7 @@
 // store; the few chunks at datagram edges are finished by their owning lane.
 // No MFMA: there is no contraction; the kernel is HBM-bound (2L+16 bytes per
 // obfuscated datagram).
-#include "salamander_wave.h"
+#include "salamander_stream.h"
 
 namespace hyobfs {
 
@@ -31,7 +31,15 @@ namespace hyobfs {
     extern template void launch_wave_sw<true, true, n>(const BatchParams&, const KeyParams&, hipStream_t);  \
     extern template void launch_wave_sw<true, false, n>(const BatchParams&, const KeyParams&, hipStream_t); \
     extern template void launch_wave_sw<false, true, n>(const BatchParams&, const KeyParams&, hipStream_t); \
-    extern template void launch_wave_sw<false, false, n>(const BatchParams&, const KeyParams&, hipStream_t);
+    extern template void launch_wave_sw<false, false, n>(const BatchParams&, const KeyParams&, hipStream_t); \
+    extern template void launch_uniform_sw<true, n>(const BatchParams&, const KeyParams&, const UniformParams&,    \
+                                                    hipStream_t);                                                  \
+    extern template void launch_uniform_sw<false, n>(const BatchParams&, const KeyParams&, const UniformParams&,   \
+                                                     hipStream_t);                                                  \
+    extern template void launch_stream_sw<true, n>(const BatchParams&, const KeyParams&, const StreamParams&,      \
+                                                   uint64_t, uint64_t, hipStream_t);                                \
+    extern template void launch_stream_sw<false, n>(const BatchParams&, const KeyParams&, const StreamParams&,     \
+                                                    uint64_t, uint64_t, hipStream_t);
 HY_EXTERN_SW(0) HY_EXTERN_SW(1) HY_EXTERN_SW(2) HY_EXTERN_SW(3) HY_EXTERN_SW(4) HY_EXTERN_SW(5)
 HY_EXTERN_SW(6) HY_EXTERN_SW(7) HY_EXTERN_SW(8) HY_EXTERN_SW(9) HY_EXTERN_SW(10) HY_EXTERN_SW(11)
 HY_EXTERN_SW(12) HY_EXTERN_SW(13) HY_EXTERN_SW(14) HY_EXTERN_SW(15)
@@ -141,18 +149,28 @@ __global__ void synth_bimodal_kernel(uint32_t* dst, uint64_t n, uint64_t seed, u
 // wave-group kernel (salamander_wave.h), packed batches the persistent
 // workgroup kernel (salamander_device.h), which handles the boundary-heavy
 // ragged mixes better.  HYOBFS_KERNEL=wave|persistent forces one.
-static int kernel_override() {
-    static int v = -2;
-    if (v == -2) {
+static int kernel_override() {   // HYOBFS_KERNEL, as HYOBFS_KERNEL_* (0 = auto)
+    static int v = -1;
+    if (v == -1) {
         const char* e = std::getenv("HYOBFS_KERNEL");
-        v = !e ? -1 : std::strcmp(e, "wave") == 0 ? 1 : std::strcmp(e, "persistent") == 0 ? 0 : -1;
+        v = !e ? 0
+               : std::strcmp(e, "wave") == 0         ? 1
+               : std::strcmp(e, "persistent") == 0   ? 2
+               : std::strcmp(e, "uniform") == 0      ? 3
+               : std::strcmp(e, "stream") == 0       ? 4
+                                                      : 0;
     }
     return v;
 }
 
+static int kernel_choice(const BatchParams& bp) { return bp.kernel ? bp.kernel : kernel_override(); }
+
+int resolve_kernel(int ctx_kernel) { return ctx_kernel ? ctx_kernel : kernel_override(); }
+
 template <bool OBF, bool PACKED>
 static void launch_main(const BatchParams& bp, const KeyParams& k, hipStream_t s) {
-    const int ov = bp.kernel ? (bp.kernel == 1 ? 1 : 0) : kernel_override();
+    const int kc = kernel_choice(bp);
+    const int ov = kc == 1 ? 1 : kc == 2 ? 0 : -1;   // uniform / auto: per layout
     const bool wave = ov >= 0 ? ov == 1 : !PACKED;
     switch (k.salt_pos >> 3) {
 #define HY_CASE(n)                                    \
@@ -169,11 +187,66 @@ static void launch_main(const BatchParams& bp, const KeyParams& k, hipStream_t s
     }
 }
 
+// Uniform batches (salamander_uniform.h): the runs of two datagrams on the
+// uniform kernel; an odd last datagram through the wave kernel (its metadata
+// is reported by the uniform launch).
+template <bool OBF>
+static bool try_uniform(const BatchParams& b, const KeyParams& k, hipStream_t s) {
+    // only when asked for: on 1M x 1200 B both measure slower than the wave
+    // kernel (uniform 0.56 vs 0.50 ms, two-pass 0.47-0.62 vs 0.46)
+    const int kc = kernel_choice(b);
+    if (kc != 3 && kc != 4) return false;
+    UniformParams P;
+    StreamParams SP;
+    uint32_t W = 0;
+    if (kc == 4 && stream_params<OBF>(b, SP)) {   // two passes: keys, then one-shot sweep
+        W = SP.W;
+        switch (k.salt_pos >> 3) {
+#define HY_CASE(sw) \
+    case sw: launch_stream_sw<OBF, sw>(b, k, SP, b.n / 2, b.n, s); break;
+            HY_CASE(0) HY_CASE(1) HY_CASE(2) HY_CASE(3) HY_CASE(4) HY_CASE(5) HY_CASE(6) HY_CASE(7)
+            HY_CASE(8) HY_CASE(9) HY_CASE(10) HY_CASE(11) HY_CASE(12) HY_CASE(13) HY_CASE(14)
+            HY_CASE(15)
+#undef HY_CASE
+        }
+    } else if (uniform_params<OBF>(b, P)) {
+        W = P.W;
+        switch (k.salt_pos >> 3) {
+#define HY_CASE(n) \
+    case n: launch_uniform_sw<OBF, n>(b, k, P, s); break;
+            HY_CASE(0) HY_CASE(1) HY_CASE(2) HY_CASE(3) HY_CASE(4) HY_CASE(5) HY_CASE(6) HY_CASE(7)
+            HY_CASE(8) HY_CASE(9) HY_CASE(10) HY_CASE(11) HY_CASE(12) HY_CASE(13) HY_CASE(14)
+            HY_CASE(15)
+#undef HY_CASE
+        }
+    } else {
+        return false;
+    }
+    if (b.n & 1) {   // the odd last datagram; its metadata came with the launch above
+        const uint64_t last = b.n - 1;
+        BatchParams t = b;
+        t.n = 1;
+        t.in = b.in + last * b.in_stride;
+        if (OBF) t.salts = b.salts + last;
+        t.out = b.out + last * W;   // 16-aligned: last is even and W a multiple of 8
+        t.out_cap = W;
+        t.out_stride = W;
+        t.inv_stride = 1.0 / (double)W;
+        t.out_off = nullptr;
+        t.out_len = nullptr;
+        t.out_total = nullptr;
+        t.kernel = 1;
+        launch_main<OBF, false>(t, k, s);
+    }
+    return true;
+}
+
 hipError_t launch_salamander(bool obf, const BatchParams& b, const KeyParams& k, hipStream_t s) {
     if (b.n == 0) return hipSuccess;
     const uint64_t ntiles = div_up(b.n, kTile);
     if (ntiles > 0x7fffffffull) return hipErrorInvalidValue;
     if (k.nblk == 2 && (k.salt_pos >> 3) != 15) return hipErrorInvalidValue;   // by construction
+    if (obf ? try_uniform<true>(b, k, s) : try_uniform<false>(b, k, s)) return hipGetLastError();
     BatchParams bp = b;
     if (b.out_stride == 0) {
         const dim3 grid((uint32_t)ntiles), block(kTile);

@@ -1,6 +1,6 @@
 // salamander_inst.hip -- instantiates the main kernel for one salt word
 // (compiled once per HY_SW = 0..15, see Makefile).
-#include "salamander_wave.h"
+#include "salamander_stream.h"
 
 #ifndef HY_SW
 #error "compile with -DHY_SW=<salt word 0..15>"
@@ -15,4 +15,10 @@ template void launch_wave_sw<true, true, HY_SW>(const BatchParams&, const KeyPar
 template void launch_wave_sw<true, false, HY_SW>(const BatchParams&, const KeyParams&, hipStream_t);
 template void launch_wave_sw<false, true, HY_SW>(const BatchParams&, const KeyParams&, hipStream_t);
 template void launch_wave_sw<false, false, HY_SW>(const BatchParams&, const KeyParams&, hipStream_t);
+template void launch_uniform_sw<true, HY_SW>(const BatchParams&, const KeyParams&, const UniformParams&, hipStream_t);
+template void launch_uniform_sw<false, HY_SW>(const BatchParams&, const KeyParams&, const UniformParams&, hipStream_t);
+template void launch_stream_sw<true, HY_SW>(const BatchParams&, const KeyParams&, const StreamParams&, uint64_t,
+                                            uint64_t, hipStream_t);
+template void launch_stream_sw<false, HY_SW>(const BatchParams&, const KeyParams&, const StreamParams&, uint64_t,
+                                             uint64_t, hipStream_t);
 }  // namespace hyobfs

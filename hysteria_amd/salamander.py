@@ -136,10 +136,10 @@ class SalamanderObfuscator:
     def __exit__(self, *exc):
         self.close()
 
-    KERNELS = {"auto": 0, "wave": 1, "persistent": 2}
+    KERNELS = {"auto": 0, "wave": 1, "persistent": 2, "uniform": 3, "stream": 4}
 
     def set_kernel(self, kernel: str) -> None:
-        """Batch kernel of this context: "auto" (per layout), "wave" or "persistent"."""
+        """Batch kernel of this context: "auto" (per layout), "wave", "persistent", "uniform" or "stream"."""
         check(self._lib.hyobfs_salamander_set_kernel(self._h, self.KERNELS[kernel]), "set_kernel")
 
     # ------------------------------------------------------------ salt source

@@ -90,10 +90,24 @@ void hyobfs_salamander_free(hyobfs_salamander* ctx);
 int hyobfs_salamander_device(const hyobfs_salamander* ctx);
 
 /* Batch kernel of this context (no reference counterpart: a tuning knob).
-   HYOBFS_KERNEL_AUTO picks per layout (slotted -> wave-group kernel, packed ->
-   persistent kernel; the HYOBFS_KERNEL environment variable overrides AUTO).
-   Returns HYOBFS_ERR_INVALID for an unknown value.  Outputs are identical. */
-enum { HYOBFS_KERNEL_AUTO = 0, HYOBFS_KERNEL_WAVE = 1, HYOBFS_KERNEL_PERSISTENT = 2 };
+   HYOBFS_KERNEL_AUTO picks per layout: slotted batches -> wave-group kernel,
+   packed batches -> persistent kernel.  For uniform batches (equal lengths, a
+   multiple of 8, payloads of 512 B or more, dense 16-aligned input and
+   output, nothing dropped) two more kernels can be asked for:
+   HYOBFS_KERNEL_UNIFORM (aligned-load sweep over runs of two datagrams) and
+   HYOBFS_KERNEL_STREAM (keys pass into context scratch pipelined with one-shot
+   4 KiB sweeps); both measure slower than AUTO on 1M x 1200 B.  The
+   HYOBFS_KERNEL environment variable (wave|persistent|uniform|stream)
+   overrides AUTO.  UNIFORM or STREAM on a batch that is not uniform falls back
+   to the AUTO choice.  Returns HYOBFS_ERR_INVALID for an unknown value.
+   Outputs are identical. */
+enum {
+    HYOBFS_KERNEL_AUTO = 0,
+    HYOBFS_KERNEL_WAVE = 1,
+    HYOBFS_KERNEL_PERSISTENT = 2,
+    HYOBFS_KERNEL_UNIFORM = 3,
+    HYOBFS_KERNEL_STREAM = 4
+};
 int hyobfs_salamander_set_kernel(hyobfs_salamander* ctx, int kernel);
 
 /* Salt source (the reference's RandSrc, salamander.go:29,43,65).  The context

@@ -63,9 +63,11 @@ int64_t hyobfs_conn_read_from(hyobfs_conn* c, uint8_t* p, size_t cap, void* addr
 /* WriteTo: len on success (also for the empty-datagram quirk), -1 with errno set. */
 int64_t hyobfs_conn_write_to(hyobfs_conn* c, const uint8_t* p, size_t len, const void* addr,
                              uint32_t addrlen);
-/* Receive up to n valid datagrams (blocks for the first; invalid ones, and
-   empty datagrams that ReadFrom would return as a 0-byte read, are dropped).
-   Returns the count (>= 0), or -1 with errno set. */
+/* Receive up to n datagrams (blocks for the first).  Invalid ones (len <= 8
+   or larger than the entry's cap) are dropped, as ReadFrom drops them; an
+   empty datagram is returned as an entry with len 0, as ReadFrom returns it
+   as a 0-byte read (conn.go:77-80).  Returns the count (>= 0), or -1 with
+   errno set. */
 int hyobfs_conn_read_batch(hyobfs_conn* c, hyobfs_dgram* msgs, uint32_t n);
 /* Obfuscate and send n datagrams with one GPU batch.  Returns the count sent,
    or -1 with errno set. */

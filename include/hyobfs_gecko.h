@@ -101,8 +101,9 @@ typedef struct hyobfs_gecko_batch {
     uint8_t* out;                        /* device */
     const uint64_t* out_off;             /* frame i's wire datagram at out + out_off[i] (device);
                                             its length is 8 + 5 + pad_len + chunk_len */
-    void* workspace;                     /* >= hyobfs_gecko_workspace_size(n) bytes (device);
-                                            reserved: the kernel derives keys in registers */
+    void* workspace;                     /* >= hyobfs_gecko_workspace_size(n) bytes (device); the
+                                            shipped kernel derives keys in registers, so the
+                                            size is 0 and NULL is accepted */
     uint64_t workspace_bytes;
 } hyobfs_gecko_batch;
 
@@ -115,7 +116,7 @@ uint64_t hyobfs_gecko_workspace_size(uint64_t n);
  * not have produced (total chunks outside [2, 8], chunk index >= total, or a
  * datagram longer than HYOBFS_GECKO_BUFFER_SIZE) is skipped on the device: its
  * output bytes are left untouched.  HYOBFS_ERR_INVALID for a missing pointer
- * or a short workspace.
+ * or a workspace shorter than hyobfs_gecko_workspace_size(n).
  */
 int hyobfs_gecko_encode_batch(hyobfs_salamander* ctx, const hyobfs_gecko_batch* b, void* stream);
 

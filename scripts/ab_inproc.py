@@ -12,13 +12,17 @@ import torch  # noqa: E402
 
 from hysteria_amd import _lib  # noqa: E402
 
-libs = sys.argv[1:] or ["hysteria_amd/libhyobfs.so"]
+# each argument: path/to/lib.so[:kernel]  (kernel = auto|wave|persistent|uniform)
+KERNELS = {"auto": 0, "wave": 1, "persistent": 2, "uniform": 3, "stream": 4}
+specs = [a.split(":") for a in (sys.argv[1:] or ["hysteria_amd/libhyobfs.so"])]
+libs = [x[0] for x in specs]
 P, L = 1 << 20, int(os.environ.get("AB_LEN", "1200"))
 workload = os.environ.get("AB_WORKLOAD", "uniform")
 dev = torch.device("cuda:0")
 main = _lib.load(os.path.abspath(libs[0]))
 handles = []
-for path in libs:
+for spec in specs:
+    path = spec[0]
     lib = ctypes.CDLL(os.path.abspath(path))
     lib.hyobfs_salamander_new.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int,
                                           ctypes.POINTER(ctypes.c_void_p)]
@@ -27,7 +31,9 @@ for path in libs:
     h = ctypes.c_void_p()
     psk = b"average_password"
     assert lib.hyobfs_salamander_new(psk, len(psk), 0, ctypes.byref(h)) == 0
-    handles.append((os.path.basename(path), lib, h))
+    kern = spec[1] if len(spec) > 1 else "auto"
+    assert lib.hyobfs_salamander_set_kernel(h, KERNELS[kern]) == 0
+    handles.append((os.path.basename(path).replace("libhyobfs_", "").replace(".so", "") + ":" + kern, lib, h))
 
 if workload == "uniform":
     inp = torch.empty(P * L, dtype=torch.uint8, device=dev)

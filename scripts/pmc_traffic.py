@@ -1,30 +1,70 @@
-"""HBM bytes per launch of the obfuscate kernel from rocprofv3 FETCH_SIZE and
-WRITE_SIZE passes (units: KiB).  gfx950 correction (MI355X_MICROARCH.md, HBM):
-FETCH_SIZE counts exactly half the bytes of a wide coalesced streaming read, so
-it is doubled; WRITE_SIZE is exact for 16-byte-per-lane streaming stores."""
-import csv, glob, json, os, sys
-root = sys.argv[1]
-names = set()
-def per_dispatch(counter):
-    vals = {}
-    for f in glob.glob(os.path.join(root, f"pmc_{counter}", "run_counter_collection.csv")):
+"""HBM bytes per launch of the obfuscate and deobfuscate kernels of one workload
+from rocprofv3 FETCH_SIZE and WRITE_SIZE passes (units: KiB), merged into a
+pmc_traffic.json keyed by the kernel-source hash bench.py computes.
+
+  python scripts/pmc_traffic.py <pmc dir> <uniform|bimodal> <in.json> <out.json> [source label]
+
+<pmc dir> holds pmc_FETCH_SIZE/ and pmc_WRITE_SIZE/ (scripts/collect_profiles.sh).
+gfx950 correction (MI355X_MICROARCH.md, HBM): FETCH_SIZE counts exactly half the
+bytes of a wide coalesced streaming read, so it is doubled; WRITE_SIZE is exact
+for 16-byte-per-lane streaming stores."""
+import csv, glob, json, os, re, sys
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from bench import kernel_src_sha  # noqa: E402
+
+root, wl, src, dst = sys.argv[1:5]
+label = sys.argv[5] if len(sys.argv) > 5 else root
+MAIN = {True: re.compile(r"salamander_(uniform_kernel|wave_kernel|kernel)<true"),
+        False: re.compile(r"salamander_(uniform_kernel|wave_kernel|kernel)<false")}
+
+
+def per_dispatch(counter, obf):
+    vals, names = {}, set()
+    for f in glob.glob(os.path.join(root, f"pmc_{counter}", "**", "*counter_collection.csv"), recursive=True):
         for row in csv.DictReader(open(f)):
-            if not ("salamander_kernel<true" in row["Kernel_Name"] or "salamander_wave_kernel<true" in row["Kernel_Name"]) or row["Counter_Name"] != counter:
+            if row["Counter_Name"] != counter or not MAIN[obf].search(row["Kernel_Name"]):
                 continue
             names.add(row["Kernel_Name"])
             vals[row["Dispatch_Id"]] = vals.get(row["Dispatch_Id"], 0.0) + float(row["Counter_Value"])
     v = sorted(vals.values())
-    return v[len(v) // 2] if v else None
-fetch_kib, write_kib = per_dispatch("FETCH_SIZE"), per_dispatch("WRITE_SIZE")
-P, L = 1 << 20, 1200
-fetch = 2 * fetch_kib * 1024
-write = write_kib * 1024
-alg = P * (2 * L + 16)
-print(json.dumps({
-    "kernel": " | ".join(sorted(names)), "datagrams": P, "len": L,
-    "fetch_size_kib_raw": fetch_kib, "write_size_kib": write_kib,
-    "hbm_read_bytes_per_launch": fetch, "hbm_write_bytes_per_launch": write,
-    "hbm_bytes_per_launch": fetch + write, "algorithmic_bytes_per_launch": alg,
-    "traffic_over_algorithmic": (fetch + write) / alg,
-    "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes), median dispatch, FETCH_SIZE x2 (gfx950)",
-}, indent=1))
+    return (v[len(v) // 2] if v else None), names
+
+
+if wl == "uniform":
+    P, L = 1 << 20, 1200
+    alg = {True: P * (2 * L + 16), False: P * (2 * L + 8)}
+else:
+    from oracle.salamander_ref import COracle
+    P, L = 1 << 22, "bimodal"
+    total_in = int(COracle().bimodal_lengths(3, 0, P).sum(dtype="uint64"))
+    alg = {True: 2 * total_in + 16 * P, False: 2 * total_in + 8 * P}
+sha = kernel_src_sha()
+try:
+    entries = json.load(open(src)).get("entries", [])
+except (OSError, ValueError, AttributeError):
+    entries = []
+for obf in (True, False):
+    direction = "obfuscate" if obf else "deobfuscate"
+    fetch_kib, n1 = per_dispatch("FETCH_SIZE", obf)
+    write_kib, n2 = per_dispatch("WRITE_SIZE", obf)
+    if fetch_kib is None or write_kib is None:
+        print(f"no {direction} dispatches in {root}", file=sys.stderr)
+        continue
+    fetch, write = 2 * fetch_kib * 1024, write_kib * 1024
+    entries = [e for e in entries if not (e.get("src_sha") == sha and e.get("workload") == wl
+                                          and e.get("direction") == direction)]
+    entries.append({
+        "src_sha": sha, "workload": wl, "direction": direction, "datagrams": P, "len": L,
+        "kernel": " | ".join(sorted(n1 | n2)), "fetch_size_kib_raw": fetch_kib, "write_size_kib": write_kib,
+        "hbm_read_bytes_per_launch": fetch, "hbm_write_bytes_per_launch": write,
+        "hbm_bytes_per_launch": fetch + write, "algorithmic_bytes_per_launch": alg[obf],
+        "traffic_over_algorithmic": round((fetch + write) / alg[obf], 4),
+        # algorithmic reads: obfuscate L + 8 (payload, salt), deobfuscate L + 8 (wire)
+        "read_over_algorithmic_read": round(fetch / ((alg[obf] + (0 if obf else 8 * P)) / 2), 4),
+        "write_over_algorithmic_write": round(write / ((alg[obf] - (0 if obf else 8 * P)) / 2), 4),
+        "source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes), median dispatch, "
+                  f"FETCH_SIZE x2 (gfx950); {label}"})
+json.dump({"note": "HBM bytes per launch keyed by kernel_src_sha (bench.py); regenerate with "
+                   "scripts/collect_profiles.sh on the tree being measured", "entries": entries},
+          open(dst, "w"), indent=1)
+print(json.dumps(entries[-2:], indent=1))

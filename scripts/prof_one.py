@@ -1,12 +1,16 @@
 """Minimal driver for rocprofv3 counter passes: K obfuscate + K deobfuscate launches
-of the uniform 1M x 1200 B batch (BASELINE configs[1]), or bimodal with 'bimodal'."""
+of the uniform 1M x 1200 B batch (BASELINE configs[1]), or of the 4M bimodal
+batch (configs[2], packed output) with 'bimodal'.  Optional 3rd argument: the
+context's kernel (auto|wave|persistent|uniform)."""
 import os, sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch, hysteria_amd
 wl = sys.argv[1] if len(sys.argv) > 1 else "uniform"
 K = int(sys.argv[2]) if len(sys.argv) > 2 else 5
+kern = sys.argv[3] if len(sys.argv) > 3 else "auto"
 dev = torch.device("cuda:0")
 o = hysteria_amd.SalamanderObfuscator(b"average_password", 0)
+o.set_kernel(kern)
 if wl == "uniform":
     P, L = 1 << 20, 1200
     inp = torch.empty(P * L, dtype=torch.uint8, device=dev); hysteria_amd.synth_stream(inp, P * L, 1, 0)
@@ -25,7 +29,15 @@ else:
     salts = torch.empty(P, dtype=torch.int64, device=dev); hysteria_amd.synth_u64(salts, P, 2, 0)
     cap = total_in + 8 * P
     wire = torch.empty(cap, dtype=torch.uint8, device=dev)
+    out_off = torch.empty(P, dtype=torch.int64, device=dev)
+    out_len = torch.empty(P, dtype=torch.int32, device=dev)
+    back = torch.empty(total_in + 16, dtype=torch.uint8, device=dev)
+    ws = torch.empty(hysteria_amd.workspace_size(P), dtype=torch.uint8, device=dev)
     for _ in range(K):
-        o.obfuscate_batch(inp, P, in_off=in_off, in_len=lens, salts=salts, out=wire, out_cap=cap)
+        o.obfuscate_batch(inp, P, in_off=in_off, in_len=lens, salts=salts, out=wire, out_cap=cap,
+                          out_off=out_off, out_len=out_len, workspace=ws, workspace_bytes=ws.numel())
+    for _ in range(K):
+        o.deobfuscate_batch(wire, P, in_off=out_off, in_len=out_len, out=back, out_cap=total_in,
+                            workspace=ws, workspace_bytes=ws.numel())
 torch.cuda.synchronize()
-print("done", wl, K)
+print("done", wl, K, kern)

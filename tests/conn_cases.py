@@ -98,14 +98,18 @@ def run_conn_scenarios(device: int = 0, batch: int = 64, n_batch: int = 200):
                     assert wire == ref.obfuscate(PSK, p, wire[:8], len(p) + 8)
         assert sent == n_batch
 
-        # batched: WriteBatch -> ReadBatch; invalid and empty datagrams are dropped
-        expect = [p for p in pays if 1 <= len(p) <= 2040]
+        # batched: WriteBatch -> ReadBatch; invalid datagrams (the 8-byte salt-only
+        # one of an empty payload, junk) are dropped, and an empty datagram (the
+        # > 2040-byte quirk) is a 0-byte entry, as ReadFrom returns it (conn.go:77-80)
+        def seen(p):
+            return p if len(p) <= 2040 else b""
+        expect = [seen(p) for p in pays if len(p) >= 1]
         got = []
         for i in range(0, n_batch, 32):
             grp = pays[i:i + 32]
             assert ca.write_batch([(p, b_addr) for p in grp]) == len(grp)
             raw.sendto(b"x" * 8, b_addr)   # junk between groups
-            want = sum(1 for p in grp if 1 <= len(p) <= 2040)
+            want = sum(1 for p in grp if len(p) >= 1)
             have = 0
             while have < want:
                 msgs = cb.read_batch(64)

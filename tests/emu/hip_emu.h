@@ -152,6 +152,8 @@ inline uint32_t hyemu_alignbit(uint32_t hi, uint32_t lo, uint32_t s) {
 }
 #define __builtin_amdgcn_alignbit(a, b, c) hyemu_alignbit((a), (b), (c))
 
+inline uint32_t __umulhi(uint32_t a, uint32_t b) { return (uint32_t)(((uint64_t)a * b) >> 32); }
+
 template <class T>
 inline T min(T a, T b) { return a < b ? a : b; }
 template <class T>

@@ -122,19 +122,38 @@ def main():
         return {"n": n, "lens": "bimodal(seed=3)", "in_bytes": total_in,
                 "obf_sha256": hashlib.sha256(wire.tobytes()).hexdigest()}
 
+    def shard_digest(first, n, L, chunk=1 << 18):
+        """One rank's shard of the configs[3] batch (64M x 1200 B over 8 GPUs): datagrams
+        [first, first + n) of the global synthetic batch, obfuscated into dense slots,
+        digested chunk by chunk (the whole shard is ~10 GB)."""
+        h = hashlib.sha256()
+        threads = os.cpu_count() or 1
+        for q in range(first, first + n, chunk):
+            m = min(chunk, first + n - q)
+            inp = co.fill_stream(1, q * L, m * L)
+            salts = co.salts(2, q, m)
+            wire = np.empty(m * (L + 8), np.uint8)
+            co.run_uniform(True, psk, m, inp, L, L, salts, wire, L + 8, threads)
+            h.update(wire.tobytes())
+        return {"first": first, "n": n, "len": L, "obf_sha256": h.hexdigest()}
+
     out["config1_cpu_10k_x_1200"] = uniform_digest(10_000, 1200)
     out["small_64k_x_1200"] = uniform_digest(65_536, 1200)
     out["bimodal_64k"] = bimodal_digest(65_536)
+    large = ("config2_1M_x_1200", "config3_bimodal_4M", "config4_shard7_8M_x_1200")
     if "--large" in sys.argv:
         out["config2_1M_x_1200"] = uniform_digest(1 << 20, 1200)
         out["config3_bimodal_4M"] = bimodal_digest(1 << 22)
+        out["config4_shard7_8M_x_1200"] = shard_digest(7 << 23, 1 << 23, 1200)
     else:
         old = os.path.join(HERE, "batch_digests.json")
         if os.path.exists(old):
             prev = json.load(open(old))
-            for k in ("config2_1M_x_1200", "config3_bimodal_4M"):
+            for k in large:
                 if k in prev:
                     out[k] = prev[k]
+        if "--shard" in sys.argv:
+            out["config4_shard7_8M_x_1200"] = shard_digest(7 << 23, 1 << 23, 1200)
     out["definition"] = ("payload = SplitMix64(seed=1) LE byte stream packed; salts = SplitMix64(seed=2) "
                          "outputs LE; bimodal len_i = 64 if SplitMix64(seed=3)_i % 5 < 2 else 1350; "
                          "PSK = average_password; digest = SHA-256 of the packed wire (obfuscate)")

@@ -67,6 +67,39 @@ RUN_CASES = [
 ]
 
 
+# The uniform kernel (salamander_uniform.h): equal lengths, multiples of 8, dense
+# slots, payloads of 512 B and more; odd counts (the last datagram through the
+# wave kernel), odd word counts (1192), the shortest eligible runs (512 B
+# payloads: 65 chunks per run), several blocks (3000), and lengths that are not
+# eligible (1201, 504, 8, 16: the wave kernel).
+UNIFORM_CASES = [
+    ("uniform", "257 1200 1"), ("uniform", "256 1200 0"), ("uniform", "301 1192 1"),
+    ("uniform", "301 1192 0"), ("uniform", "300 512 1"), ("uniform", "300 512 0"),
+    ("uniform", "129 1400 1"), ("uniform", "3001 1200 0"), ("uniform", "3000 1200 1"),
+    ("uniform", "99 1201 1"), ("uniform", "99 504 1"), ("uniform", "129 8 0"), ("uniform", "64 16 1"),
+]
+
+
+@pytest.mark.parametrize("which,args", UNIFORM_CASES)
+def test_emulated_uniform_kernel(emu_lib, which, args):
+    _run(emu_lib, which, args, {"HYOBFS_KERNEL": "uniform", "HYEMU_CUS": "2"})
+
+
+@pytest.mark.parametrize("which,args", UNIFORM_CASES)
+def test_emulated_stream_kernel(emu_lib, which, args):
+    """The two-pass path (salamander_stream.h): keys into the context's scratch, then
+    one-shot waves over contiguous chunk regions (same cases as the uniform kernel)."""
+    _run(emu_lib, which, args, {"HYOBFS_KERNEL": "stream", "HYEMU_CUS": "2"})
+
+
+@pytest.mark.parametrize("args", ["3001 1200 0", "3000 1200 1", "2999 1192 1", "1000 512 0"])
+def test_emulated_stream_kernel_pipelined(emu_lib, args):
+    """Many chunks (first chunk 40 runs, doubling): every launch sweeps one chunk and
+    keys the next; region carries across chunk ends."""
+    _run(emu_lib, "uniform", args, {"HYOBFS_KERNEL": "stream", "HYEMU_CUS": "2",
+                                    "HYOBFS_STREAM_FIRST_RUNS": "40", "HYOBFS_STREAM_GROW": "2"})
+
+
 def _run(emu_lib, which, args, extra_env):
     env = dict(os.environ, HYOBFS_LIB=emu_lib, LD_PRELOAD=_asan_runtime(), ASAN_OPTIONS="detect_leaks=0",
                **extra_env)

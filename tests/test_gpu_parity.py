@@ -17,10 +17,13 @@ pytestmark = pytest.mark.gpu
 PSK = b"average_password"
 
 
-@pytest.fixture(scope="module", params=["auto", "wave", "persistent"])
+@pytest.fixture(scope="module", params=["auto", "wave", "persistent", "uniform", "stream"])
 def obfs(gpu, request):
     """One context per batch kernel: auto (the shipped per-layout choice), and
-    each kernel forced on every layout (salamander_wave.h, salamander_device.h)."""
+    each kernel forced on every layout (salamander_wave.h, salamander_device.h;
+    the uniform and two-pass stream kernels, salamander_uniform.h and
+    salamander_stream.h, apply to uniform batches and fall back to the auto
+    choice elsewhere)."""
     import hysteria_amd
     o = hysteria_amd.SalamanderObfuscator(PSK, 0)
     o.set_kernel(request.param)
@@ -181,6 +184,87 @@ def test_config2_1M_x_1200_digest_and_roundtrip(obfs, gpu, golden):
     obfs.deobfuscate_batch(out, n, in_stride=L + 8, len_uniform=L + 8, out=back, out_stride=L)
     torch.cuda.synchronize()
     assert torch.equal(back, inp[: n * L])
+
+
+def test_config4_shard7_8M_x_1200_digest_and_roundtrip(gpu, golden):
+    """BASELINE configs[3] (64M x 1200 B over 8 GPUs): the shard rank 7 owns,
+    datagrams [7*8M, 8*8M) of the global synthetic batch, generated at that offset
+    and obfuscated through the product as one 8M batch; digest committed by
+    gen_golden.py from the C oracle; device round trip."""
+    import torch
+    import hysteria_amd
+    d = golden[1]["config4_shard7_8M_x_1200"]
+    first, n, L = d["first"], d["n"], d["len"]
+    inp = torch.empty(n * L, dtype=torch.uint8, device=gpu)
+    hysteria_amd.synth_stream(inp, n * L, 1, first * L)
+    salts = torch.empty(n, dtype=torch.int64, device=gpu)
+    hysteria_amd.synth_u64(salts, n, 2, first)
+    out = torch.empty(n * (L + 8), dtype=torch.uint8, device=gpu)
+    with hysteria_amd.SalamanderObfuscator(PSK, 0) as o:
+        o.obfuscate_batch(inp, n, in_stride=L, len_uniform=L, salts=salts, out=out, out_stride=L + 8)
+        torch.cuda.synchronize()
+        h = hashlib.sha256()
+        step = 1 << 28
+        for s in range(0, out.numel(), step):
+            h.update(out[s:s + step].cpu().numpy().tobytes())
+        assert h.hexdigest() == d["obf_sha256"]
+        back = torch.empty(n * L, dtype=torch.uint8, device=gpu)
+        o.deobfuscate_batch(out, n, in_stride=L + 8, len_uniform=L + 8, out=back, out_stride=L)
+        torch.cuda.synchronize()
+        assert torch.equal(back, inp)
+
+
+def test_concurrent_packed_batches_one_context(gpu, coracle):
+    """hyobfs.h promises a context may be used from several threads: two host
+    threads, each on its own stream, submit 50 packed ragged batches of changing
+    sizes through ONE context with no caller workspace (the context's per-stream
+    scratch, grown while the other thread's kernels run).  Every output against
+    the oracle."""
+    import threading
+    import torch
+    import hysteria_amd
+    nmax = 20_000
+    lens, in_off, inp, salts, total_in = _bimodal(gpu, nmax)
+    h_lens, h_off, h_inp = _host(lens).view(np.uint32), _host(in_off).view(np.uint64), _host(inp)
+    h_salts = coracle.salts(2, 0, nmax)
+    sizes = {0: [500, 3000, 20_000, 1000, 12_000], 1: [17_000, 700, 9000, 20_000, 2500]}
+    want = {}
+    for n in set(sizes[0] + sizes[1]):
+        cap = int(h_lens[:n].astype(np.uint64).sum()) + 8 * n
+        exp, _, _, _ = coracle.batch(True, PSK, n, h_inp, in_off=h_off[:n], in_len=h_lens[:n], salts=h_salts[:n],
+                                     out_cap=cap)
+        want[n] = exp
+    results = {0: [], 1: []}
+    errors = []
+    with hysteria_amd.SalamanderObfuscator(PSK, 0) as o:
+        o.set_kernel("persistent")   # packed ragged: the kernel behind the tile-sum scratch
+
+        def worker(t):
+            try:
+                s = torch.cuda.Stream(device=gpu)
+                with torch.cuda.stream(s):
+                    for i in range(50):
+                        n = sizes[t][i % 5]
+                        cap = want[n].size
+                        out = torch.empty(cap, dtype=torch.uint8, device=gpu)
+                        o.obfuscate_batch(inp, n, in_off=in_off, in_len=lens, salts=salts, out=out, out_cap=cap,
+                                          stream=s)
+                        results[t].append((n, out))
+                s.synchronize()
+            except Exception as e:   # reported from the main thread
+                errors.append(e)
+
+        th = [threading.Thread(target=worker, args=(t,)) for t in (0, 1)]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join()
+        torch.cuda.synchronize()
+    assert not errors, errors
+    for t in (0, 1):
+        assert len(results[t]) == 50
+        for i, (n, out) in enumerate(results[t]):
+            assert np.array_equal(_host(out), want[n]), (t, i, n)
 
 
 def _bimodal(gpu, n):
