@@ -17,7 +17,7 @@ for wl in uniform bimodal; do
       python3 "$R/scripts/prof_one.py" $wl 5 > "$O/$wl.pmc_$c.log" 2>&1 || { echo "pmc $wl $c failed"; exit 1; }
   done
   python3 "$R/scripts/pmc_traffic.py" "$O/$wl" $wl "$O/pmc_traffic.json" "$O/pmc_traffic.json" \
-    "profiles/${TAG}_pmc_$wl" > "$O/pmc_$wl.txt" || { echo "pmc_traffic $wl failed"; exit 1; }
+    "profiles/${TAG}_pmc/${wl}_{FETCH,WRITE}_SIZE.csv" > "$O/pmc_$wl.txt" || { echo "pmc_traffic $wl failed"; exit 1; }
 done
 # 2. kernel trace + stats of the bench command itself
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/kt" -o run -- \
