@@ -117,6 +117,9 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         "hyobfs_conn_write_to": (ctypes.c_int64, [vp, vp, sz, vp, u32]),
         "hyobfs_conn_read_batch": (i32, [vp, vp, u32]),
         "hyobfs_conn_write_batch": (i32, [vp, vp, u32]),
+        "hyobfs_conn_set_coalescing": (i32, [vp, u32, u32]),
+        "hyobfs_conn_flush": (i32, [vp]),
+        "hyobfs_conn_stats": (i32, [vp, ctypes.POINTER(ctypes.c_uint64)]),
         "hyobfs_synth_stream": (i32, [vp, u64, u64, u64, vp]),
         "hyobfs_synth_u64": (i32, [vp, u64, u64, u64, vp]),
         "hyobfs_synth_bimodal_lengths": (i32, [vp, u64, u64, u64, vp]),

@@ -15,6 +15,8 @@ reference (Go)                             here
 ``Set{,Read,Write}Deadline``               ``settimeout(seconds)`` (SO_RCVTIMEO/SO_SNDTIMEO)
 ``SetReadBuffer`` / ``SetWriteBuffer``     ``set_read_buffer`` / ``set_write_buffer``
 (new) batched receive / send               ``read_batch(n)`` / ``write_batch(msgs)``
+(new) coalescing per-datagram calls        ``set_coalescing(max_batch, max_wait_us)``,
+                                           ``flush()``, ``stats()``
 =========================================  ==========================================
 
 Kept reference behaviour: ``read_from`` drops datagrams that fail to
@@ -97,8 +99,6 @@ class SalamanderPacketConn:
         check(self._lib.hyobfs_conn_wrap(sock.fileno(), obfuscator._h, batch, ctypes.byref(h)), "hyobfs_conn_wrap")
         self._h = h
         self.batch = batch
-        self._rbuf = ctypes.create_string_buffer(UDP_BUFFER_SIZE)
-        self._addr = ctypes.create_string_buffer(128)
 
     # ------------------------------------------------------------ lifecycle
     def close(self) -> None:
@@ -142,12 +142,14 @@ class SalamanderPacketConn:
 
     def read_from(self, bufsize: int = UDP_BUFFER_SIZE):
         """ReadFrom (conn.go:73-88): (payload, addr) of the next valid datagram."""
-        buf = self._rbuf if bufsize <= UDP_BUFFER_SIZE else ctypes.create_string_buffer(bufsize)
+        # per-call buffers: several threads may read one connection at once
+        buf = ctypes.create_string_buffer(max(bufsize, 1))
+        addr = ctypes.create_string_buffer(128)
         al = ctypes.c_uint32(128)
-        n = self._lib.hyobfs_conn_read_from(self._h, buf, bufsize, self._addr, ctypes.byref(al))
+        n = self._lib.hyobfs_conn_read_from(self._h, buf, bufsize, addr, ctypes.byref(al))
         if n < 0:
             _raise_errno("read")
-        return buf.raw[:n], _pyaddr(self._addr.raw[: al.value])
+        return buf.raw[:n], _pyaddr(addr.raw[: al.value])
 
     def write_to(self, p, addr) -> int:
         """WriteTo (conn.go:90-99): returns len(p); > 2040 bytes sends an empty datagram."""
@@ -157,6 +159,22 @@ class SalamanderPacketConn:
         if n < 0:
             _raise_errno("write")
         return n
+
+    # ------------------------------------------------------------ coalescing
+    def set_coalescing(self, max_batch: int = 1024, max_wait_us: int = 50) -> None:
+        """Serve the per-datagram write_to / read_from from GPU batches (include/hyobfs_conn.h,
+        hyobfs_conn_set_coalescing): write_to returns once the datagram is queued; many
+        threads may call both.  The batched calls are unavailable afterwards."""
+        check(self._lib.hyobfs_conn_set_coalescing(self._h, max_batch, max_wait_us), "set_coalescing")
+
+    def flush(self) -> None:
+        """Wait until every datagram write_to accepted was handed to the socket."""
+        check(self._lib.hyobfs_conn_flush(self._h), "flush")
+
+    def stats(self) -> dict:
+        out = (ctypes.c_uint64 * 6)()
+        check(self._lib.hyobfs_conn_stats(self._h, out), "stats")
+        return dict(zip(("accepted", "tx_batches", "tx_errors", "received", "rx_batches", "rx_dropped"), out))
 
     # ------------------------------------------------------------ batched
     def read_batch(self, n: int, bufsize: int = UDP_BUFFER_SIZE):

@@ -1,0 +1,452 @@
+// conn_coalesce.cpp -- batching behind the per-datagram WriteTo / ReadFrom of a
+// coalescing hyobfs_conn (include/hyobfs_conn.h, hyobfs_conn_set_coalescing).
+//
+// The reference calls Obfuscate / Deobfuscate once per datagram inside
+// obfsPacketConn.WriteTo / ReadFrom (extras/obfs/conn.go:73-99); a GPU call per
+// datagram is a PCIe round trip.  Here many callers' datagrams share one GPU
+// batch:
+//   * send: WriteTo reserves a slot in the filling batch (a short spin lock),
+//     copies the datagram and returns len(p).  A flusher thread seals the batch
+//     when it is full or max_wait_us after its first datagram, obfuscates it on
+//     the GPU (pinned staging, hyobfs_salamander_obfuscate_host) and sends it
+//     with sendmmsg, while the next batch fills.  Like a UDP sendto, the call
+//     returns once the datagram is queued; a later send failure is counted, not
+//     reported to that caller.
+//   * receive: a reader thread receives up to max_batch datagrams with
+//     recvmmsg, deobfuscates them in one GPU batch and queues the batch;
+//     ReadFrom takes the next datagram from the queue.  Datagrams that do not
+//     deobfuscate are dropped and an empty datagram is a 0-byte read, as in
+//     ReadFrom (conn.go:77-86).  The socket's SO_RCVTIMEO bounds the wait.
+#include "conn_coalesce.h"
+
+#include <errno.h>
+#include <poll.h>
+#include <string.h>
+#include <sys/socket.h>
+#include <sys/time.h>
+
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <deque>
+#include <mutex>
+#include <new>
+#include <thread>
+#include <vector>
+
+#include "../../include/hyobfs_conn.h"
+
+namespace hyobfs {
+namespace {
+
+constexpr uint32_t kBuf = HYOBFS_UDP_BUFFER_SIZE;   // udpBufferSize, conn.go:10
+using Clock = std::chrono::steady_clock;
+
+struct Pinned {   // device-mapped pinned slots of kBuf bytes
+    uint8_t* in = nullptr;
+    uint8_t* out = nullptr;
+    uint32_t* len = nullptr;
+    uint32_t* olen = nullptr;
+    uint64_t* salts = nullptr;
+    bool alloc(uint32_t n) {
+        in = static_cast<uint8_t*>(hyobfs_host_alloc((size_t)n * kBuf));
+        out = static_cast<uint8_t*>(hyobfs_host_alloc((size_t)n * kBuf));
+        len = static_cast<uint32_t*>(hyobfs_host_alloc((size_t)n * 4));
+        olen = static_cast<uint32_t*>(hyobfs_host_alloc((size_t)n * 4));
+        salts = static_cast<uint64_t*>(hyobfs_host_alloc((size_t)n * 8));
+        return in && out && len && olen && salts;
+    }
+    void release() {
+        hyobfs_host_free(in);
+        hyobfs_host_free(out);
+        hyobfs_host_free(len);
+        hyobfs_host_free(olen);
+        hyobfs_host_free(salts);
+    }
+};
+
+struct Batch {
+    Pinned b;
+    std::vector<sockaddr_storage> addr;
+    std::vector<uint32_t> alen;
+    std::vector<mmsghdr> msg;
+    std::vector<iovec> iov;
+    // send side (count / sealed / first under the spin lock)
+    uint32_t count = 0;
+    bool sealed = false;
+    Clock::time_point first{};
+    std::atomic<uint32_t> committed{0};
+    // receive side (k / next under rx_mu)
+    uint32_t k = 0, next = 0;
+    std::atomic<uint32_t> done{0};
+    bool alloc(uint32_t n) {
+        addr.resize(n);
+        alen.resize(n);
+        msg.resize(n);
+        iov.resize(n);
+        return b.alloc(n);
+    }
+};
+
+class Spin {
+    std::atomic_flag f = ATOMIC_FLAG_INIT;
+
+   public:
+    void lock() {
+        while (f.test_and_set(std::memory_order_acquire)) std::this_thread::yield();
+    }
+    void unlock() { f.clear(std::memory_order_release); }
+};
+
+}  // namespace
+
+struct Coalescer {
+    int fd = -1;
+    hyobfs_salamander* ctx = nullptr;
+    uint32_t max_batch = 0;
+    std::chrono::microseconds max_wait{0};
+    std::atomic<bool> stop{false};
+    // send
+    Batch tx[2];
+    int cur = 0;                         // filling batch, under spin
+    Spin spin;
+    std::mutex tx_mu;                    // waits: flusher for datagrams, writers for space
+    std::condition_variable cv_flush, cv_space;
+    std::atomic<uint64_t> accepted{0}, sent{0}, tx_batches{0}, tx_errors{0};
+    std::thread flusher;
+    // receive
+    Batch rx[3];
+    std::mutex rx_mu;
+    std::condition_variable cv_ready, cv_free;
+    std::deque<int> ready, freelist;
+    int rx_err = 0;
+    std::atomic<uint64_t> received{0}, rx_batches{0}, rx_dropped{0};
+    std::thread reader;
+
+    bool has_space() const { return !tx[cur].sealed && tx[cur].count < max_batch; }
+    void flush_loop();
+    void send_batch(Batch& b, uint32_t n);
+    void read_loop();
+};
+
+void Coalescer::send_batch(Batch& b, uint32_t n) {
+    hyobfs_salamander_next_salts(ctx, reinterpret_cast<uint8_t*>(b.b.salts), n);   // RandSrc, salamander.go:65
+    hyobfs_batch d{};
+    d.n = n;
+    d.in = b.b.in;
+    d.in_stride = kBuf;
+    d.in_len = b.b.len;
+    d.salts = b.b.salts;
+    d.out = b.b.out;
+    d.out_stride = kBuf;   // len(writeBuf): Obfuscate needs len + 8 <= 2048, else an empty datagram
+    d.out_cap = (uint64_t)n * kBuf;
+    d.out_len = b.b.olen;
+    if (hyobfs_salamander_obfuscate_host(ctx, &d, 0) != HYOBFS_OK) {
+        tx_errors += n;
+        sent += n;   // handled (lost): flush() must not wait for them
+        return;
+    }
+    for (uint32_t i = 0; i < n; ++i) {
+        b.iov[i].iov_base = b.b.out + (size_t)i * kBuf;
+        b.iov[i].iov_len = b.b.olen[i];
+        memset(&b.msg[i], 0, sizeof(mmsghdr));
+        b.msg[i].msg_hdr.msg_iov = &b.iov[i];
+        b.msg[i].msg_hdr.msg_iovlen = 1;
+        b.msg[i].msg_hdr.msg_name = &b.addr[i];
+        b.msg[i].msg_hdr.msg_namelen = b.alen[i];
+    }
+    uint32_t done = 0;
+    while (done < n) {
+        const int r = sendmmsg(fd, b.msg.data() + done, n - done, 0);
+        if (r > 0) {
+            done += (uint32_t)r;
+            continue;
+        }
+        if (r < 0 && errno == EINTR) continue;
+        if (r < 0 && (errno == EAGAIN || errno == ENOBUFS)) {   // socket buffer full: wait for room
+            pollfd pf{fd, POLLOUT, 0};
+            (void)poll(&pf, 1, 10);
+            continue;
+        }
+        ++tx_errors;   // this datagram cannot be sent (e.g. no route): skip it
+        ++done;
+    }
+    sent += n;
+    ++tx_batches;
+}
+
+void Coalescer::flush_loop() {
+    for (;;) {
+        {
+            std::unique_lock<std::mutex> lk(tx_mu);
+            auto pending = [&] {
+                spin.lock();
+                const bool p = tx[cur].count > 0;
+                spin.unlock();
+                return p;
+            };
+            cv_flush.wait(lk, [&] { return stop.load() || pending(); });
+            if (!pending()) return;   // stopping, nothing left to send
+            spin.lock();
+            const Clock::time_point deadline = tx[cur].first + max_wait;
+            spin.unlock();
+            cv_flush.wait_until(lk, deadline, [&] {
+                spin.lock();
+                const bool full = tx[cur].count >= max_batch;
+                spin.unlock();
+                return full || stop.load();
+            });
+            // seal the filling batch; writers move on to the other one (already sent)
+            spin.lock();
+            Batch& b = tx[cur];
+            b.sealed = true;
+            cur ^= 1;
+            spin.unlock();
+        }
+        cv_space.notify_all();
+        Batch& b = tx[cur ^ 1];
+        const uint32_t n = b.count;   // no writer changes a sealed batch's count
+        while (b.committed.load(std::memory_order_acquire) < n) std::this_thread::yield();
+        send_batch(b, n);
+        spin.lock();
+        b.count = 0;
+        b.committed.store(0, std::memory_order_relaxed);
+        b.sealed = false;
+        spin.unlock();
+        {
+            std::lock_guard<std::mutex> lk(tx_mu);   // writers waiting for space re-check under tx_mu
+        }
+        cv_space.notify_all();
+    }
+}
+
+void Coalescer::read_loop() {
+    for (;;) {
+        int bi;
+        {
+            std::unique_lock<std::mutex> lk(rx_mu);
+            cv_free.wait(lk, [&] { return stop.load() || !freelist.empty(); });
+            if (stop) return;
+            bi = freelist.front();
+            freelist.pop_front();
+        }
+        Batch& b = rx[bi];
+        int k = -1;
+        while (!stop) {
+            pollfd pf{fd, POLLIN, 0};
+            const int pr = poll(&pf, 1, 50);
+            if (pr <= 0) continue;   // timeout or EINTR: check stop, poll again
+            for (uint32_t i = 0; i < max_batch; ++i) {
+                b.iov[i].iov_base = b.b.in + (size_t)i * kBuf;
+                b.iov[i].iov_len = kBuf;
+                memset(&b.msg[i], 0, sizeof(mmsghdr));
+                b.msg[i].msg_hdr.msg_iov = &b.iov[i];
+                b.msg[i].msg_hdr.msg_iovlen = 1;
+                b.msg[i].msg_hdr.msg_name = &b.addr[i];
+                b.msg[i].msg_hdr.msg_namelen = sizeof(sockaddr_storage);
+            }
+            k = recvmmsg(fd, b.msg.data(), max_batch, MSG_DONTWAIT, nullptr);
+            if (k > 0) break;
+            if (k < 0 && errno != EAGAIN && errno != EWOULDBLOCK && errno != EINTR) {
+                std::lock_guard<std::mutex> lk(rx_mu);
+                rx_err = errno;   // reported by ReadFrom once the queue is empty
+                break;
+            }
+        }
+        if (stop || k <= 0) {
+            std::lock_guard<std::mutex> lk(rx_mu);
+            freelist.push_back(bi);
+            cv_ready.notify_all();
+            if (stop) return;
+            continue;
+        }
+        for (int i = 0; i < k; ++i) {
+            b.b.len[i] = b.msg[i].msg_len;
+            b.alen[i] = b.msg[i].msg_hdr.msg_namelen;
+        }
+        hyobfs_batch d{};
+        d.n = (uint64_t)k;
+        d.in = b.b.in;
+        d.in_stride = kBuf;
+        d.in_len = b.b.len;
+        d.out = b.b.out;
+        d.out_stride = kBuf;
+        d.out_cap = (uint64_t)k * kBuf;
+        d.out_len = b.b.olen;
+        if (hyobfs_salamander_deobfuscate_host(ctx, &d, 0) != HYOBFS_OK)
+            for (int i = 0; i < k; ++i) b.b.olen[i] = 0;   // nothing deobfuscated: every datagram dropped
+        received += (uint64_t)k;
+        ++rx_batches;
+        {
+            std::lock_guard<std::mutex> lk(rx_mu);
+            b.k = (uint32_t)k;
+            b.next = 0;
+            b.done.store(0, std::memory_order_relaxed);
+            ready.push_back(bi);
+        }
+        cv_ready.notify_all();
+    }
+}
+
+Coalescer* coalescer_new(int fd, hyobfs_salamander* ctx, uint32_t max_batch, uint32_t max_wait_us) {
+    auto* q = new (std::nothrow) Coalescer();
+    if (!q) return nullptr;
+    q->fd = fd;
+    q->ctx = ctx;
+    q->max_batch = max_batch;
+    q->max_wait = std::chrono::microseconds(max_wait_us);
+    bool ok = true;
+    for (auto& b : q->tx) ok = ok && b.alloc(max_batch);
+    for (auto& b : q->rx) ok = ok && b.alloc(max_batch);
+    if (!ok) {
+        for (auto& b : q->tx) b.b.release();
+        for (auto& b : q->rx) b.b.release();
+        delete q;
+        return nullptr;
+    }
+    for (int i = 0; i < 3; ++i) q->freelist.push_back(i);
+    q->flusher = std::thread([q] { q->flush_loop(); });
+    q->reader = std::thread([q] { q->read_loop(); });
+    return q;
+}
+
+void coalescer_free(Coalescer* q) {
+    if (!q) return;
+    {
+        std::lock_guard<std::mutex> a(q->tx_mu);
+        std::lock_guard<std::mutex> b(q->rx_mu);
+        q->stop = true;
+    }
+    q->cv_flush.notify_all();
+    q->cv_space.notify_all();
+    q->cv_free.notify_all();
+    q->cv_ready.notify_all();
+    q->flusher.join();   // sends what was accepted first
+    q->reader.join();
+    for (auto& b : q->tx) b.b.release();
+    for (auto& b : q->rx) b.b.release();
+    delete q;
+}
+
+int64_t coalescer_write(Coalescer* q, const uint8_t* p, size_t len, const void* addr, uint32_t addrlen) {
+    if (addrlen > sizeof(sockaddr_storage)) {
+        errno = EINVAL;
+        return -1;
+    }
+    Batch* b;
+    uint32_t idx;
+    for (;;) {
+        q->spin.lock();
+        b = &q->tx[q->cur];
+        if (q->has_space()) {
+            idx = b->count++;
+            if (idx == 0) b->first = Clock::now();
+            q->spin.unlock();
+            break;
+        }
+        q->spin.unlock();
+        std::unique_lock<std::mutex> lk(q->tx_mu);
+        q->cv_flush.notify_one();   // the filling batch is full
+        q->cv_space.wait(lk, [&] {
+            q->spin.lock();
+            const bool s = q->has_space();
+            q->spin.unlock();
+            return s || q->stop.load();
+        });
+        if (q->stop) {
+            errno = EBADF;
+            return -1;
+        }
+    }
+    // Obfuscate into a 2048-byte slot: > 2040 bytes gives out_len 0, an empty
+    // datagram, and WriteTo still reports len(p) (conn.go:92-98)
+    const uint32_t L = len > kBuf ? kBuf : (uint32_t)len;
+    if (len <= kBuf && len) memcpy(b->b.in + (size_t)idx * kBuf, p, len);
+    b->b.len[idx] = L;
+    if (addrlen) memcpy(&b->addr[idx], addr, addrlen);
+    b->alen[idx] = addrlen;
+    b->committed.fetch_add(1, std::memory_order_release);
+    ++q->accepted;
+    if (idx == 0 || idx + 1 == q->max_batch) {   // first datagram starts the wait; a full batch ends it
+        std::lock_guard<std::mutex> lk(q->tx_mu);
+        q->cv_flush.notify_one();
+    }
+    return (int64_t)len;
+}
+
+int64_t coalescer_read(Coalescer* q, uint8_t* p, size_t cap, void* addr, uint32_t* addrlen) {
+    for (;;) {
+        int bi;
+        uint32_t idx;
+        {
+            std::unique_lock<std::mutex> lk(q->rx_mu);
+            while (q->ready.empty()) {
+                if (q->rx_err) {
+                    errno = q->rx_err;
+                    q->rx_err = 0;
+                    return -1;
+                }
+                if (q->stop) {
+                    errno = EBADF;
+                    return -1;
+                }
+                timeval tv{0, 0};
+                socklen_t tl = sizeof tv;
+                (void)getsockopt(q->fd, SOL_SOCKET, SO_RCVTIMEO, &tv, &tl);   // SetReadDeadline
+                const auto t = std::chrono::seconds(tv.tv_sec) + std::chrono::microseconds(tv.tv_usec);
+                if (t.count() == 0) {
+                    q->cv_ready.wait(lk);
+                } else if (!q->cv_ready.wait_for(lk, t, [&] { return !q->ready.empty() || q->rx_err || q->stop; })) {
+                    errno = EAGAIN;
+                    return -1;
+                }
+            }
+            bi = q->ready.front();
+            Batch& b = q->rx[bi];
+            idx = b.next++;
+            if (b.next == b.k) q->ready.pop_front();
+        }
+        Batch& b = q->rx[bi];
+        const uint32_t L = b.b.len[idx], m = b.b.olen[idx];
+        const bool deliver = L == 0 || (m != 0 && m <= cap);   // empty: a 0-byte read (conn.go:77-80)
+        int64_t n = 0;
+        if (deliver) {
+            if (m && L) memcpy(p, b.b.out + (size_t)idx * kBuf, m);
+            n = L ? m : 0;
+            if (addr && addrlen) {
+                const uint32_t al = b.alen[idx] < *addrlen ? b.alen[idx] : *addrlen;
+                memcpy(addr, &b.addr[idx], al);
+                *addrlen = b.alen[idx];
+            }
+        } else {
+            ++q->rx_dropped;   // Deobfuscate returned 0: dropped, read on (conn.go:86)
+        }
+        if (b.done.fetch_add(1, std::memory_order_acq_rel) + 1 == b.k) {
+            std::lock_guard<std::mutex> lk(q->rx_mu);
+            q->freelist.push_back(bi);
+            q->cv_free.notify_one();
+        }
+        if (deliver) return n;
+    }
+}
+
+int coalescer_flush(Coalescer* q) {
+    const uint64_t target = q->accepted.load();
+    {
+        std::lock_guard<std::mutex> lk(q->tx_mu);
+        q->cv_flush.notify_one();
+    }
+    while (q->sent.load() < target) std::this_thread::sleep_for(std::chrono::microseconds(20));
+    return HYOBFS_OK;
+}
+
+void coalescer_stats(const Coalescer* q, uint64_t out[6]) {
+    out[0] = q->accepted.load();
+    out[1] = q->tx_batches.load();
+    out[2] = q->tx_errors.load();
+    out[3] = q->received.load();
+    out[4] = q->rx_batches.load();
+    out[5] = q->rx_dropped.load();
+}
+
+}  // namespace hyobfs

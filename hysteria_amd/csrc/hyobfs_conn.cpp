@@ -3,6 +3,8 @@
 // See include/hyobfs_conn.h for the reference mapping and kept behaviour.
 #include "../../include/hyobfs_conn.h"
 
+#include "conn_coalesce.h"
+
 #include <errno.h>
 #include <string.h>
 #include <sys/socket.h>
@@ -55,6 +57,7 @@ struct hyobfs_conn {
     std::vector<mmsghdr> rmsg, wmsg;
     std::vector<iovec> riov, wiov;
     std::vector<sockaddr_storage> raddr;
+    hyobfs::Coalescer* co = nullptr;       // set: per-datagram calls go through batches
 };
 
 extern "C" {
@@ -83,6 +86,7 @@ int hyobfs_conn_wrap(int fd, hyobfs_salamander* ctx, uint32_t batch, hyobfs_conn
 
 void hyobfs_conn_free(hyobfs_conn* c) {
     if (!c) return;
+    hyobfs::coalescer_free(c->co);   // sends what WriteTo accepted, stops its threads
     c->rx.release();
     c->tx.release();
     delete c;
@@ -101,6 +105,7 @@ int64_t hyobfs_conn_read_from(hyobfs_conn* c, uint8_t* p, size_t cap, void* addr
         errno = EINVAL;
         return -1;
     }
+    if (c->co) return hyobfs::coalescer_read(c->co, p, cap, addr, addrlen);
     for (;;) {
         std::lock_guard<std::mutex> lk(c->read_mu);
         socklen_t al = addrlen ? *addrlen : 0;
@@ -119,6 +124,7 @@ int64_t hyobfs_conn_write_to(hyobfs_conn* c, const uint8_t* p, size_t len, const
         errno = EINVAL;
         return -1;
     }
+    if (c->co) return hyobfs::coalescer_write(c->co, p, len, addr, addrlen);
     std::lock_guard<std::mutex> lk(c->write_mu);
     // Obfuscate into the 2048-byte writeBuf: 0 when len > 2040 (salamander.go:60-62)
     const size_t nn = hyobfs_salamander_obfuscate_auto(c->ctx, p, len, c->write_buf, kBuf);
@@ -133,6 +139,10 @@ int hyobfs_conn_read_batch(hyobfs_conn* c, hyobfs_dgram* msgs, uint32_t n) {
         return -1;
     }
     if (n == 0) return 0;
+    if (c->co) {   // the coalescer's reader owns the socket's receive side
+        errno = EBUSY;
+        return -1;
+    }
     std::lock_guard<std::mutex> lk(c->read_mu);
     n = std::min(n, c->rx.n);
     for (;;) {
@@ -184,6 +194,10 @@ int hyobfs_conn_write_batch(hyobfs_conn* c, const hyobfs_dgram* msgs, uint32_t n
         errno = EINVAL;
         return -1;
     }
+    if (c->co) {
+        errno = EBUSY;
+        return -1;
+    }
     std::lock_guard<std::mutex> lk(c->write_mu);
     uint32_t sent = 0;
     while (sent < n) {
@@ -228,6 +242,27 @@ int hyobfs_conn_write_batch(hyobfs_conn* c, const hyobfs_dgram* msgs, uint32_t n
         sent += k;
     }
     return (int)sent;
+}
+
+int hyobfs_conn_set_coalescing(hyobfs_conn* c, uint32_t max_batch, uint32_t max_wait_us) {
+    if (!c || c->co || max_batch == 0 || max_batch > (1u << 16)) return HYOBFS_ERR_INVALID;
+    c->co = hyobfs::coalescer_new(c->fd, c->ctx, max_batch, max_wait_us);
+    return c->co ? HYOBFS_OK : HYOBFS_ERR_NOMEM;
+}
+
+int hyobfs_conn_flush(hyobfs_conn* c) {
+    if (!c) return HYOBFS_ERR_INVALID;
+    return c->co ? hyobfs::coalescer_flush(c->co) : HYOBFS_OK;
+}
+
+int hyobfs_conn_stats(hyobfs_conn* c, uint64_t out[6]) {
+    if (!c || !out) return HYOBFS_ERR_INVALID;
+    if (!c->co) {
+        for (int i = 0; i < 6; ++i) out[i] = 0;
+        return HYOBFS_OK;
+    }
+    hyobfs::coalescer_stats(c->co, out);
+    return HYOBFS_OK;
 }
 
 }  // extern "C"

@@ -382,14 +382,18 @@ def workspace_size(n: int) -> int:
     return int(_glib().hyobfs_gecko_workspace_size(n))
 
 
-def encode_batch(obfuscator, *, msg, frames, salts, pad_seed: int, out, out_off, workspace, n=None,
+def encode_batch(obfuscator, *, msg, frames, salts, pad_seed: int, out, out_off, workspace=None, n=None,
                  stream=None) -> None:
     """hyobfs_gecko_encode_batch: every frame's wire datagram in one device pass.
-    Arguments are device tensors (torch) or device pointers."""
+    Arguments are device tensors (torch) or device pointers; the shipped kernel
+    needs no workspace (workspace_size() == 0)."""
     from .salamander import _ptr, _stream
     if n is None:   # frames: 16-byte hyobfs_gecko_frame records
         n = frames.numel() * frames.element_size() // FRAME_DTYPE.itemsize if hasattr(frames, "numel") else len(frames)
-    ws_bytes = workspace.numel() * workspace.element_size() if hasattr(workspace, "numel") else workspace_size(n)
+    if workspace is None:
+        ws_bytes = 0
+    else:
+        ws_bytes = workspace.numel() * workspace.element_size() if hasattr(workspace, "numel") else workspace_size(n)
     b = HyobfsGeckoBatch(n=n, msg=_ptr(msg), frames=_ptr(frames), salts=_ptr(salts), pad_seed=pad_seed,
                          out=_ptr(out), out_off=_ptr(out_off), workspace=_ptr(workspace), workspace_bytes=ws_bytes)
     check(_glib().hyobfs_gecko_encode_batch(obfuscator._h, ctypes.byref(b), _stream(stream, out)), "gecko_encode_batch")

@@ -73,6 +73,30 @@ int hyobfs_conn_read_batch(hyobfs_conn* c, hyobfs_dgram* msgs, uint32_t n);
    or -1 with errno set. */
 int hyobfs_conn_write_batch(hyobfs_conn* c, const hyobfs_dgram* msgs, uint32_t n);
 
+/* Coalescing mode (no reference counterpart: a throughput knob behind the
+   unchanged per-datagram surface, conn.go:73-99).  After this call:
+     - hyobfs_conn_write_to copies the datagram into the filling batch and
+       returns len(p) at once (the > 2040-byte quirk included).  A flusher
+       thread seals the batch when it holds max_batch datagrams or max_wait_us
+       after its first one, obfuscates it as one GPU batch and sends it with
+       sendmmsg while the next batch fills.  Like a UDP sendto, a datagram is
+       accepted once queued; a later send failure is counted in the stats, not
+       returned.  Writers block while both batches are busy (backpressure).
+     - hyobfs_conn_read_from is served from batches a reader thread receives
+       with recvmmsg and deobfuscates as one GPU batch: invalid datagrams are
+       dropped and an empty datagram is a 0-byte read, as ReadFrom does; the
+       socket's SO_RCVTIMEO bounds the wait (-1, errno EAGAIN).
+     - many threads may call write_to / read_from at once; the batched calls
+       return -1 with errno EBUSY.
+   Latency added per datagram: up to max_wait_us plus one GPU batch.  Call once,
+   before the connection is used; hyobfs_conn_free / _close send what was
+   accepted, then stop the threads. */
+int hyobfs_conn_set_coalescing(hyobfs_conn* c, uint32_t max_batch, uint32_t max_wait_us);
+/* Blocks until every datagram write_to accepted so far was handed to the socket. */
+int hyobfs_conn_flush(hyobfs_conn* c);
+/* Coalescing counters: accepted, tx batches, tx errors, received, rx batches, rx dropped. */
+int hyobfs_conn_stats(hyobfs_conn* c, uint64_t out[6]);
+
 #ifdef __cplusplus
 }
 #endif

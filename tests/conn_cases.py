@@ -5,6 +5,7 @@ Shared by the CPU-emulated tier (tests/emu/run_case.py conn) and the GPU tier
 (oracle/salamander_ref.py); the reference's own conn behaviour being checked is
 cited per step.
 """
+import errno
 import socket
 
 import numpy as np
@@ -138,6 +139,126 @@ def run_conn_scenarios(device: int = 0, batch: int = 64, n_batch: int = 200):
         try:
             cb.read_batch(8)
             raise AssertionError("read_batch did not time out")
+        except TimeoutError:
+            pass
+    finally:
+        ca.close()
+        cb.close()
+        raw.close()
+        oa.close()
+        ob.close()
+
+
+def run_coalesce_scenarios(device: int = 0, writers: int = 8, per_writer: int = 300, readers: int = 4,
+                           max_batch: int = 64, max_wait_us: int = 200):
+    """Coalescing mode (hyobfs_conn_set_coalescing): many threads calling the
+    per-datagram WriteTo / ReadFrom of one connection share GPU batches.  Every
+    datagram arrives exactly once with the reference's per-datagram semantics
+    (conn.go:73-99): wire bytes equal the oracle's, invalid datagrams are
+    dropped, an empty datagram is a 0-byte read, a > 2040-byte payload goes out
+    as an empty datagram, the read deadline holds."""
+    import threading
+    rng = np.random.default_rng(17)
+    sa, sb, raw = _udp(), _udp(), _udp()
+    for s in (sa, sb, raw):
+        s.setsockopt(socket.SOL_SOCKET, socket.SO_RCVBUF, 32 << 20)
+        s.setsockopt(socket.SOL_SOCKET, socket.SO_SNDBUF, 32 << 20)
+    oa, ob = SalamanderObfuscator(PSK, device), SalamanderObfuscator(PSK, device)
+    ca, cb = SalamanderPacketConn(sa, oa, batch=max_batch), SalamanderPacketConn(sb, ob, batch=max_batch)
+    ca.set_coalescing(max_batch, max_wait_us)
+    cb.set_coalescing(max_batch, max_wait_us)
+    a_addr, b_addr, r_addr = ca.local_addr(), cb.local_addr(), raw.getsockname()
+    try:
+        # the batched calls belong to the coalescer now
+        for call in (lambda: ca.write_batch([(b"x", b_addr)]), lambda: cb.read_batch(4)):
+            try:
+                call()
+                raise AssertionError("batched call allowed in coalescing mode")
+            except OSError as e:
+                assert e.errno == errno.EBUSY
+
+        # many writers -> many readers: each payload carries (writer, seq); lengths
+        # include 0 (an 8-byte datagram the reader drops) and 2041 (an empty datagram)
+        def payload(w, i):
+            n = [0, 1, 9, 100, 1200, 2040, 2041, 31][i % 8] if i < 16 else 16 + (w * 131 + i * 17) % 1400
+            head = bytes([w]) + i.to_bytes(3, "little")
+            return (head * (n // 4 + 1))[:n]
+        expect = {}
+        for w in range(writers):
+            for i in range(per_writer):
+                p = payload(w, i)
+                if len(p) == 0:
+                    continue                      # salt-only datagram: dropped by the reader
+                key = p if len(p) <= 2040 else b""
+                expect[key] = expect.get(key, 0) + 1
+        total = sum(expect.values())
+        got, lock = {}, threading.Lock()
+        cb.settimeout(3.0)   # readers left over once every datagram arrived end on this
+
+        def reader():
+            while True:
+                with lock:
+                    if sum(got.values()) >= total:
+                        return
+                try:
+                    m, addr = cb.read_from()
+                except TimeoutError:
+                    return
+                assert addr == a_addr
+                with lock:
+                    got[m] = got.get(m, 0) + 1
+
+        def writer(w):
+            for i in range(per_writer):
+                p = payload(w, i)
+                assert ca.write_to(p, b_addr) == len(p)
+
+        rt = [threading.Thread(target=reader) for _ in range(readers)]
+        wt = [threading.Thread(target=writer, args=(w,)) for w in range(writers)]
+        for t in rt + wt:
+            t.start()
+        for t in wt:
+            t.join()
+        ca.flush()
+        for t in rt:
+            t.join()
+        if got != expect:
+            extra = {(k[:8].hex(), len(k)): (v, expect.get(k)) for k, v in got.items() if expect.get(k) != v}
+            miss = {(k[:8].hex(), len(k)): (v, got.get(k)) for k, v in expect.items() if got.get(k) != v}
+            raise AssertionError((sum(got.values()), total, list(extra.items())[:5], list(miss.items())[:5]))
+        st = ca.stats()
+        assert st["accepted"] == writers * per_writer and st["tx_errors"] == 0 and st["tx_batches"] >= 1
+
+        # wire bytes against the oracle (coalescing writer -> plain socket)
+        sent = [_payload(rng, n) for n in (0, 1, 33, 1200, 2040, 2041)]
+        for p in sent:
+            ca.write_to(p, r_addr)
+        ca.flush()
+        seen = []
+        for _ in sent:
+            wire, addr = raw.recvfrom(4096)
+            assert addr == a_addr
+            seen.append(wire)
+        for p in sent:   # one batch: sendmmsg keeps the order
+            wire = seen.pop(0)
+            if len(p) > 2040:
+                assert wire == b""
+            else:
+                assert wire == ref.obfuscate(PSK, p, wire[:8], len(p) + 8), len(p)
+
+        # plain socket -> coalescing reader: junk dropped, empty datagram = 0-byte read
+        raw.sendto(b"12345678", b_addr)
+        q = _payload(rng, 60)
+        raw.sendto(ref.obfuscate(PSK, q, b"\x02" * 8, 68), b_addr)
+        raw.sendto(b"", b_addr)
+        assert cb.read_from() == (q, r_addr)
+        assert cb.read_from() == (b"", r_addr)
+        assert cb.stats()["rx_dropped"] >= 1
+        # SetReadDeadline: an idle read times out
+        cb.settimeout(0.2)
+        try:
+            cb.read_from()
+            raise AssertionError("read did not time out")
         except TimeoutError:
             pass
     finally:

@@ -10,6 +10,7 @@ mkdir -p build
 $CXX $FLAGS -c $SRC/salamander.hip -o build/salamander.o &
 $CXX $FLAGS -c $SRC/hyobfs_api.cpp -o build/hyobfs_api.o &
 $CXX $FLAGS -c $SRC/hyobfs_conn.cpp -o build/hyobfs_conn.o &
+$CXX $FLAGS -c $SRC/conn_coalesce.cpp -o build/conn_coalesce.o &
 $CXX $FLAGS -c $SRC/gecko.hip -o build/gecko.o &
 $CXX $FLAGS -c $SRC/realm.hip -o build/realm.o &
 $CXX $FLAGS -c $SRC/gecko_host.cpp -o build/gecko_host.o &

@@ -45,6 +45,7 @@ CASES = [
     ("host", "1000 300 96 1", "2"),      # host-resident batch, chunked pipeline
     ("host", "1000 300 96 0", "2"),
     ("conn", "64 120", "2"),             # UDP loopback through the conn wrapper (conn.go)
+    ("coalesce", "8 150 4 32", "2"),     # many threads on one coalescing conn (hyobfs_conn_set_coalescing)
     ("far", "200 300 15 1", "8"),        # workgroup bases beyond 2^31
     ("far", "200 300 15 0", "8"),
     ("gecko", "40 7", "2"),              # Gecko frame encode + parse kernels (gecko.hip)
@@ -124,7 +125,7 @@ def test_emulated_wave_kernel_packed_run_lengths(emu_lib, which, args, run_log2)
 @pytest.mark.parametrize("which,args,cus", CASES)
 def test_emulated_persistent_kernel(emu_lib, which, args, cus):
     """The persistent workgroup kernel (HYOBFS_KERNEL=persistent) on the same cases."""
-    if which in ("conn", "host"):
+    if which in ("conn", "host", "coalesce"):
         pytest.skip("kernel-independent host paths run once, under the default kernel")
     _run(emu_lib, which, args, {"HYEMU_CUS": cus, "HYOBFS_KERNEL": "persistent"})
 

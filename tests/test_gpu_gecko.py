@@ -203,3 +203,74 @@ def test_gecko_over_salamander_udp_loopback(gpu):
     finally:
         ga.close()
         gb.close()
+
+
+def test_encode_kernel_frame_grid(gpu):
+    """TestEncodeDecodeFrame (gecko_frame_test.go:9-42) through the DEVICE encoder:
+    totals 2..8, every chunk index, pad lengths 0/1/64/127/512/1100, payload
+    a1 b2 c3 d4, msg id 0xa5.  Every wire datagram deobfuscates (oracle) and
+    decodes (decodeFrame restated) to the same header and payload, and equals the
+    oracle's wire byte for byte.  No workspace is passed (the shipped kernel needs none)."""
+    import torch
+    import hysteria_amd
+    from hysteria_amd import gecko
+    payload = bytes([0xA1, 0xB2, 0xC3, 0xD4])
+    grid = [(t, i, pad) for t in range(2, 9) for i in range(t) for pad in (0, 1, 64, 127, 512, 1100)]
+    fr = np.array([(0, len(payload), pad, 0xA5, (i << 4) | t) for t, i, pad in grid], dtype=gecko.FRAME_DTYPE)
+    wl = 8 + 5 + fr["pad_len"].astype(np.uint64) + len(payload)
+    off = np.concatenate([[0], np.cumsum(wl)[:-1]]).astype(np.uint64)
+    total = int(wl.sum())
+    salts = sref.splitmix64_array(21, 0, len(fr))
+    msg = np.frombuffer(payload + b"\0" * 12, np.uint8)
+    o = hysteria_amd.SalamanderObfuscator(PSK, 0)
+    try:
+        out = torch.full((total + 64,), 0xA5, dtype=torch.uint8, device=gpu)
+        gecko.encode_batch(o, msg=_dev(msg, gpu), frames=_dev(fr, gpu), salts=_dev(salts, gpu), pad_seed=99,
+                           out=out, out_off=_dev(off, gpu), n=len(fr))
+        got = out.cpu().numpy()
+    finally:
+        o.close()
+    assert got[total:].tobytes() == b"\xa5" * 64
+    exp = gref.encode_wire(PSK, msg.tobytes(), fr.tolist(), salts, 99)
+    for k, (t, i, pad) in enumerate(grid):
+        wire = got[int(off[k]):int(off[k]) + int(wl[k])].tobytes()
+        assert wire == exp[k], (t, i, pad)
+        plain = sref.deobfuscate(PSK, wire)
+        h, body = gref.decode_frame(plain)
+        assert (h.pad_len, h.msg_id, h.chunk_idx, h.total_chunks) == (pad, 0xA5, i, t), (t, i, pad)
+        assert body == payload
+
+
+# TestDecodeFrameRejectsInvalid (gecko_frame_test.go:77-96) through the DEVICE parser.
+# The parser classifies as ReadFrom does (gecko.go:176-193): an empty datagram is
+# skipped before decodeFrame (EMPTY) and a clear top bit is passed through (PASS);
+# every datagram with the top bit set gets decodeFrame's verdict.
+DECODE_REJECTS = [
+    ("empty", b"", "EMPTY"),
+    ("header truncated", bytes([0x80, 0x55, 0x22, 0x00]), "ERR_TRUNCATED"),
+    ("not a fragment", bytes([0x00, 0x00, 0x22, 0x00, 0x00]), "PASS"),
+    ("totalChunks zero", bytes([0x80, 0x00, 0x00, 0x00, 0x00]), "ERR_INVALID"),
+    ("totalChunks one", bytes([0x80, 0x00, 0x01, 0x00, 0x00]), "ERR_INVALID"),
+    ("totalChunks nine", bytes([0x80, 0x00, 0x09, 0x00, 0x00]), "ERR_INVALID"),
+    ("chunkIdx == totalChunks", bytes([0x80, 0x00, 0x44, 0x00, 0x00]), "ERR_INVALID"),
+    ("padLen overrun", bytes([0x80, 0x00, 0x02, 0x00, 0x12, 0x01, 0x02]), "ERR_TRUNCATED"),
+]
+
+
+def test_parse_kernel_decode_frame_rejects(gpu):
+    import torch
+    from hysteria_amd import gecko
+    data = b"".join(d for _, d, _ in DECODE_REJECTS)
+    lens = np.array([len(d) for _, d, _ in DECODE_REJECTS], np.uint32)
+    offs = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.uint64)
+    n = len(lens)
+    parsed = torch.empty(n * 16, dtype=torch.uint8, device=gpu)
+    gecko.parse_batch(_dev(np.frombuffer(data + b"\0" * 16, np.uint8), gpu), _dev(offs, gpu).view(torch.int64),
+                      _dev(lens, gpu).view(torch.int32), n, parsed)
+    torch.cuda.synchronize()
+    pr = parsed.cpu().numpy().view(gecko.PARSED_DTYPE)
+    oracle_status = {gref.PASS: gecko.PASS, gref.FRAGMENT: gecko.FRAGMENT, gref.EMPTY: gecko.EMPTY,
+                     gref.TRUNCATED: gecko.ERR_TRUNCATED, gref.INVALID: gecko.ERR_INVALID}
+    for k, (name, d, want) in enumerate(DECODE_REJECTS):
+        assert int(pr[k]["status"]) == getattr(gecko, want), name
+        assert int(pr[k]["status"]) == oracle_status[gref.parse(d)[0]], name

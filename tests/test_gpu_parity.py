@@ -509,6 +509,14 @@ def test_packet_conn_loopback(gpu):
     run_conn_scenarios(device=0, batch=1024, n_batch=400)
 
 
+@pytest.mark.gpu
+def test_packet_conn_coalescing_loopback(gpu):
+    """Coalescing mode: 8 writer and 4 reader threads on the per-datagram calls of one
+    connection each side, GPU batches behind them; wire bytes against the oracle."""
+    from conn_cases import run_coalesce_scenarios
+    run_coalesce_scenarios(device=0, writers=8, per_writer=1000, readers=4, max_batch=256, max_wait_us=100)
+
+
 # ------------------------------------------------------------- sharded batches
 @pytest.mark.parametrize("nshards", [1, 2, 3])
 def test_sharded_batch_matches_single_batch(gpu, coracle, nshards):

@@ -4,11 +4,15 @@
 // deobfuscate with hyobfs_conn_read_batch (recvmmsg + one GPU batch).
 // Every received payload is checked (sequence number + content tag).
 //
-//   udp_bench [mode=batch|single|raw] [pairs=4] [seconds=5] [len=1200] [batch=1024]
+//   udp_bench [mode=batch|single|raw|coalesce] [pairs=4] [seconds=5] [len=1200] [batch=1024]
+//             [threads=2] [wait_us=50]
 //
 // "raw" sends and receives the same datagrams with plain sendmmsg/recvmmsg and no
 // obfuscation: the loopback socket ceiling.  "single" uses WriteTo/ReadFrom, one
 // GPU round trip per datagram, the shape of the reference's obfsPacketConn.
+// "coalesce" keeps that per-datagram shape (WriteTo / ReadFrom, `threads`
+// writer and `threads` reader threads per pair) on coalescing connections
+// (hyobfs_conn_set_coalescing: GPU batches of up to `batch` behind the calls).
 // Prints one JSON line.
 #include <arpa/inet.h>
 #include <netinet/in.h>
@@ -80,7 +84,9 @@ int main(int argc, char** argv) {
     const uint32_t len = argc > 4 ? (uint32_t)atoi(argv[4]) : 1200;
     const uint32_t batch = argc > 5 ? (uint32_t)atoi(argv[5]) : 1024;
     const uint8_t psk[] = "udp_bench_password";
-    const bool raw = mode == "raw", single = mode == "single";
+    const int threads = argc > 6 ? atoi(argv[6]) : 2;
+    const uint32_t wait_us = argc > 7 ? (uint32_t)atoi(argv[7]) : 50;
+    const bool raw = mode == "raw", coalesce = mode == "coalesce", single = mode == "single" || coalesce;
     if (len < 16 || len > 2040) {
         fprintf(stderr, "len must be in [16, 2040]\n");
         return 2;
@@ -95,6 +101,8 @@ int main(int argc, char** argv) {
             if (st == HYOBFS_OK) st = hyobfs_salamander_new(psk, sizeof psk - 1, 0, &p.rctx);
             if (st == HYOBFS_OK) st = hyobfs_conn_wrap(p.sfd, p.sctx, batch, &p.sc);
             if (st == HYOBFS_OK) st = hyobfs_conn_wrap(p.rfd, p.rctx, batch, &p.rc);
+            if (st == HYOBFS_OK && coalesce) st = hyobfs_conn_set_coalescing(p.sc, batch, wait_us);
+            if (st == HYOBFS_OK && coalesce) st = hyobfs_conn_set_coalescing(p.rc, batch, wait_us);
             if (st != HYOBFS_OK) {
                 fprintf(stderr, "setup: %s\n", hyobfs_status_string(st));
                 return 1;
@@ -104,9 +112,11 @@ int main(int argc, char** argv) {
 
     std::atomic<bool> stop{false}, rstop{false};
     std::vector<std::thread> th;
-    for (int pi = 0; pi < pairs; ++pi) {
+    const int per_side = coalesce ? threads : 1;
+    for (int pi = 0; pi < pairs; ++pi)
+      for (int ti = 0; ti < per_side; ++ti) {
         Pair& p = P[pi];
-        th.emplace_back([&, pi] {   // sender
+        th.emplace_back([&, pi, ti] {   // sender
             std::vector<uint8_t> buf((size_t)batch * len);
             std::vector<hyobfs_dgram> d(batch);
             std::vector<mmsghdr> mh(batch);
@@ -123,7 +133,7 @@ int main(int argc, char** argv) {
                 mh[i].msg_hdr.msg_name = &p.raddr;
                 mh[i].msg_hdr.msg_namelen = sizeof p.raddr;
             }
-            uint64_t seq = (uint64_t)pi << 48;
+            uint64_t seq = (uint64_t)pi << 48 | (uint64_t)ti << 40;
             while (!stop.load(std::memory_order_relaxed)) {
                 for (uint32_t i = 0; i < batch; ++i) fill(d[i].buf, len, seq++);
                 if (single) {
@@ -205,10 +215,10 @@ int main(int argc, char** argv) {
         hyobfs_salamander_free(p.rctx);
     }
     const double rx = (double)(r1 - r0), tx = (double)(s1 - s0);
-    printf("{\"mode\": \"%s\", \"pairs\": %d, \"len\": %u, \"batch\": %u, \"seconds\": %.3f, "
+    printf("{\"mode\": \"%s\", \"pairs\": %d, \"threads_per_side\": %d, \"wait_us\": %u, \"len\": %u, \"batch\": %u, \"seconds\": %.3f, "
            "\"rx_datagrams_per_s\": %.0f, \"tx_datagrams_per_s\": %.0f, \"rx_payload_GiB_s\": %.4f, "
            "\"tx_payload_GiB_s\": %.4f, \"loss_frac\": %.4f, \"bad\": %llu, \"avg_per_read\": %.1f}\n",
-           mode.c_str(), pairs, len, batch, dt, rx / dt, tx / dt, rx * len / dt / (1u << 30), tx * len / dt / (1u << 30),
+           mode.c_str(), pairs, per_side, coalesce ? wait_us : 0u, len, batch, dt, rx / dt, tx / dt, rx * len / dt / (1u << 30), tx * len / dt / (1u << 30),
            sent ? 1.0 - (double)recvd / (double)sent : 0.0, (unsigned long long)bad,
            calls ? (double)recvd / (double)calls : 0.0);
     return bad ? 1 : 0;
