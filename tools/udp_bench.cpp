@@ -20,7 +20,9 @@
 #include <sys/socket.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <atomic>
+#include <mutex>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -32,10 +34,21 @@
 
 static uint64_t tag(uint64_t seq) { return seq * 0x9E3779B97F4A7C15ull ^ 0xD1B54A32D192ED03ull; }
 
+static uint64_t now_ns() {
+    return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+               std::chrono::steady_clock::now().time_since_epoch())
+        .count();
+}
+
+// payload: sequence number, send time (steady clock, ns), then the sequence's tag
 static void fill(uint8_t* p, uint32_t len, uint64_t seq) {
     memcpy(p, &seq, 8);
     const uint64_t t = tag(seq);
-    for (uint32_t o = 8; o + 8 <= len; o += 8) memcpy(p + o, &t, 8);
+    for (uint32_t o = 16; o + 8 <= len; o += 8) memcpy(p + o, &t, 8);
+}
+static void stamp(uint8_t* p) {
+    const uint64_t ts = now_ns();
+    memcpy(p + 8, &ts, 8);
 }
 
 static bool check(const uint8_t* p, uint32_t len, uint32_t want_len) {
@@ -43,7 +56,7 @@ static bool check(const uint8_t* p, uint32_t len, uint32_t want_len) {
     uint64_t seq;
     memcpy(&seq, p, 8);
     const uint64_t t = tag(seq);
-    for (uint32_t o = 8; o + 8 <= len; o += 8)
+    for (uint32_t o = 16; o + 8 <= len; o += 8)
         if (memcmp(p + o, &t, 8) != 0) return false;
     return true;
 }
@@ -75,6 +88,8 @@ struct Pair {
     hyobfs_conn* sc = nullptr;
     hyobfs_conn* rc = nullptr;
     std::atomic<uint64_t> sent{0}, recvd{0}, bad{0}, calls{0};
+    std::mutex lat_mu;
+    std::vector<uint64_t> lat;   // sampled send -> receive latencies (ns)
 };
 
 int main(int argc, char** argv) {
@@ -138,9 +153,11 @@ int main(int argc, char** argv) {
                 for (uint32_t i = 0; i < batch; ++i) fill(d[i].buf, len, seq++);
                 if (single) {
                     for (uint32_t i = 0; i < batch && !stop.load(std::memory_order_relaxed); ++i) {
+                        stamp(d[i].buf);
                         if (hyobfs_conn_write_to(p.sc, d[i].buf, len, &p.raddr, sizeof p.raddr) > 0) p.sent++;
                     }
                 } else if (raw) {
+                    for (uint32_t i = 0; i < batch; ++i) stamp(d[i].buf);
                     uint32_t done = 0;
                     while (done < batch) {
                         int r = sendmmsg(p.sfd, mh.data() + done, batch - done, 0);
@@ -149,6 +166,7 @@ int main(int argc, char** argv) {
                     }
                     p.sent += done;
                 } else {
+                    for (uint32_t i = 0; i < batch; ++i) stamp(d[i].buf);
                     int r = hyobfs_conn_write_batch(p.sc, d.data(), batch);
                     if (r > 0) p.sent += r;
                 }
@@ -184,7 +202,17 @@ int main(int argc, char** argv) {
                 if (k <= 0) continue;
                 p.calls++;
                 uint64_t bad = 0;
-                for (int i = 0; i < k; ++i) bad += !check(d[i].buf, d[i].len, len);
+                const uint64_t t_rx = now_ns();
+                for (int i = 0; i < k; ++i) {
+                    bad += !check(d[i].buf, d[i].len, len);
+                    uint64_t seq, ts;
+                    memcpy(&seq, d[i].buf, 8);
+                    memcpy(&ts, d[i].buf + 8, 8);
+                    if ((seq & 63) == 0 && t_rx > ts) {   // every 64th datagram
+                        std::lock_guard<std::mutex> lk(p.lat_mu);
+                        p.lat.push_back(t_rx - ts);
+                    }
+                }
                 p.recvd += k;
                 p.bad += bad;
             }
@@ -205,6 +233,10 @@ int main(int argc, char** argv) {
     rstop = true;
     for (auto& t : th) t.join();
     uint64_t bad = 0, calls = 0, sent = 0, recvd = 0;
+    std::vector<uint64_t> lat;
+    for (auto& p : P) lat.insert(lat.end(), p.lat.begin(), p.lat.end());
+    std::sort(lat.begin(), lat.end());
+    auto pct = [&](double q) { return lat.empty() ? 0.0 : lat[(size_t)(q * (lat.size() - 1))] / 1e3; };
     for (auto& p : P) {
         bad += p.bad, calls += p.calls, sent += p.sent, recvd += p.recvd;
         if (p.sc) hyobfs_conn_free(p.sc);
@@ -217,9 +249,10 @@ int main(int argc, char** argv) {
     const double rx = (double)(r1 - r0), tx = (double)(s1 - s0);
     printf("{\"mode\": \"%s\", \"pairs\": %d, \"threads_per_side\": %d, \"wait_us\": %u, \"len\": %u, \"batch\": %u, \"seconds\": %.3f, "
            "\"rx_datagrams_per_s\": %.0f, \"tx_datagrams_per_s\": %.0f, \"rx_payload_GiB_s\": %.4f, "
-           "\"tx_payload_GiB_s\": %.4f, \"loss_frac\": %.4f, \"bad\": %llu, \"avg_per_read\": %.1f}\n",
+           "\"tx_payload_GiB_s\": %.4f, \"loss_frac\": %.4f, \"bad\": %llu, \"avg_per_read\": %.1f, "
+           "\"latency_us_p50\": %.1f, \"latency_us_p99\": %.1f, \"latency_samples\": %zu}\n",
            mode.c_str(), pairs, per_side, coalesce ? wait_us : 0u, len, batch, dt, rx / dt, tx / dt, rx * len / dt / (1u << 30), tx * len / dt / (1u << 30),
            sent ? 1.0 - (double)recvd / (double)sent : 0.0, (unsigned long long)bad,
-           calls ? (double)recvd / (double)calls : 0.0);
+           calls ? (double)recvd / (double)calls : 0.0, pct(0.5), pct(0.99), lat.size());
     return bad ? 1 : 0;
 }
