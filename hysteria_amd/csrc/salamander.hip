@@ -64,18 +64,26 @@ __global__ __launch_bounds__(kTile) void tile_sums_kernel(BatchParams B) {
     }
 }
 
-// Exclusive scan of ntiles values in place, one workgroup of 1024 threads;
-// writes the total at [ntiles].
+// Exclusive scan of ntiles values in place, one workgroup of 1024 threads,
+// each owning 16 consecutive values per pass (one pass covers 16384 tiles = 4M
+// datagrams); writes the total at [ntiles].  (A stride-1024 loop with three
+// barriers per 1024 values took 25 us for 16384 tiles.)
 __global__ __launch_bounds__(1024) void scan_tiles_kernel(uint64_t* v, uint64_t ntiles) {
+    constexpr int PER = 16;
     __shared__ uint64_t s_w[16];
     __shared__ uint64_t s_carry;
     const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
     if (t == 0) s_carry = 0;
     __syncthreads();
-    for (uint64_t base = 0; base < ntiles; base += 1024) {
-        const uint64_t i = base + t;
-        const uint64_t x = i < ntiles ? v[i] : 0;
-        const uint64_t inc = wave_incl_scan(x, lane);
+    for (uint64_t base = 0; base < ntiles; base += 1024 * PER) {
+        const uint64_t i0 = base + (uint64_t)t * PER;
+        uint64_t x[PER], sum = 0;
+#pragma unroll
+        for (int k = 0; k < PER; ++k) {
+            x[k] = i0 + k < ntiles ? v[i0 + k] : 0;
+            sum += x[k];
+        }
+        const uint64_t inc = wave_incl_scan(sum, lane);
         if (lane == 63) s_w[wid] = inc;
         __syncthreads();
         uint64_t wpre = 0, tot = 0;
@@ -85,7 +93,12 @@ __global__ __launch_bounds__(1024) void scan_tiles_kernel(uint64_t* v, uint64_t 
             tot += sw;
         }
         const uint64_t carry = s_carry;
-        if (i < ntiles) v[i] = carry + wpre + inc - x;
+        uint64_t run = carry + wpre + inc - sum;
+#pragma unroll
+        for (int k = 0; k < PER; ++k) {
+            if (i0 + k < ntiles) v[i0 + k] = run;
+            run += x[k];
+        }
         __syncthreads();
         if (t == 0) s_carry = carry + tot;
         __syncthreads();

@@ -466,6 +466,31 @@ def test_packed_output_offsets_beyond_4GiB(obfs, gpu):
         assert got == exp, p
 
 
+def test_packed_offsets_past_one_scan_pass(obfs, gpu):
+    """More than 16384 tiles (4M datagrams): the tile-sum scan takes two passes and
+    carries between them.  Packed output of 4.5M 16-byte datagrams with in_len given
+    (a ragged-batch launch): every offset and a sample of wire datagrams."""
+    import torch
+    import hysteria_amd
+    n, L = 4_500_000, 16
+    inp = torch.empty(n * L, dtype=torch.uint8, device=gpu)
+    hysteria_amd.synth_stream(inp, n * L, 1, 0)
+    lens = torch.full((n,), L, dtype=torch.int32, device=gpu)
+    in_off = torch.arange(n, dtype=torch.int64, device=gpu) * L
+    salts = torch.empty(n, dtype=torch.int64, device=gpu)
+    hysteria_amd.synth_u64(salts, n, 2, 0)
+    out = torch.empty(n * (L + 8), dtype=torch.uint8, device=gpu)
+    out_off = torch.empty(n, dtype=torch.int64, device=gpu)
+    obfs.obfuscate_batch(inp, n, in_off=in_off, in_len=lens, salts=salts, out=out, out_off=out_off)
+    torch.cuda.synchronize()
+    assert torch.equal(out_off, torch.arange(n, dtype=torch.int64, device=gpu) * (L + 8))
+    h_in = inp.cpu().numpy()
+    h_salts = salts.cpu().numpy().view(np.uint64)
+    for p in list(range(0, n, 99_991)) + [4_194_303, 4_194_304, n - 1]:
+        got = out[p * (L + 8):(p + 1) * (L + 8)].cpu().numpy().tobytes()
+        assert got == ref.obfuscate(PSK, h_in[p * L:(p + 1) * L].tobytes(), int(h_salts[p]).to_bytes(8, "little")), p
+
+
 @pytest.mark.parametrize("obf", [True, False])
 @pytest.mark.parametrize("pinned", [True, False])
 def test_host_batch_pipeline_vs_oracle(obfs, gpu, obf, pinned):
