@@ -13,6 +13,7 @@ $CXX $FLAGS -c $SRC/hyobfs_conn.cpp -o build/hyobfs_conn.o &
 $CXX $FLAGS -c $SRC/conn_coalesce.cpp -o build/conn_coalesce.o &
 $CXX $FLAGS -c $SRC/gecko.hip -o build/gecko.o &
 $CXX $FLAGS -c $SRC/realm.hip -o build/realm.o &
+$CXX $FLAGS -c $SRC/quic.hip -o build/quic.o &
 $CXX $FLAGS -c $SRC/gecko_host.cpp -o build/gecko_host.o &
 for n in $(seq 0 15); do $CXX $FLAGS -DHY_SW=$n -c $SRC/salamander_inst.hip -o build/inst_sw$n.o & done
 wait

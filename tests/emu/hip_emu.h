@@ -143,6 +143,16 @@ inline T __shfl(T v, int src, int width = 64) {
     (void)width;
     return hyemu::xchg(v, src);
 }
+inline unsigned long long __ballot(int pred) {
+    const int t = (int)threadIdx.x, w = t >> 6;
+    const int lanes = (int)std::min<uint32_t>(64, hyemu::g_blockdim.x - 64 * w);
+    hyemu::g_ctx.slots[t] = pred != 0;
+    hyemu::g_ctx.wave[w]->arrive_and_wait();
+    unsigned long long m = 0;
+    for (int l = 0; l < lanes; ++l) m |= (unsigned long long)(hyemu::g_ctx.slots[w * 64 + l] & 1) << l;
+    hyemu::g_ctx.wave[w]->arrive_and_wait();
+    return m;
+}
 // like the builtin: int in, int out (a caller that widens the result must
 // convert it to unsigned first, exactly as on the GPU)
 inline int hyemu_readfirstlane(int v) { return hyemu::xchg(v, 0); }

@@ -216,6 +216,35 @@ def case_punch(n, m, seed):
     assert 0 < hits < n
 
 
+def case_quic(seed):
+    """QUIC Initial unprotection: explicit-key UnProtect batch (both suites,
+    the reference's two vectors) and the ReadCryptoPayload batch vs the oracle."""
+    from hysteria_amd import quic
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import quic_cases as qc
+    p = lambda a: a.ctypes.data  # noqa: E731
+    cases = qc.unprotect_cases(seed)
+    buf, off, lens = qc.pack([c[2] for c in cases])
+    keys = np.frombuffer(b"".join(qc.key_record(c[1]) for c in cases), np.uint8).copy()
+    pn_off = np.array([c[3] for c in cases], np.int64)
+    pn_max = np.array([c[4] for c in cases], np.int64)
+    res = np.zeros(len(cases), quic.RESULT_DTYPE)
+    quic.unprotect_batch(p(buf), p(off), p(lens), len(cases), p(keys), p(pn_off), p(res), pn_max=p(pn_max), stream=0)
+    qc.check_unprotect(cases, buf, off, res)
+    pkts = qc.crypto_packets(seed)
+    buf, off, lens = qc.pack([x[1] for x in pkts])
+    caps = np.full(len(pkts), 2048, np.uint32)
+    caps[[i for i, x in enumerate(pkts) if x[0] == "zero_prefix"]] = 1000   # -51 path
+    out_off = np.concatenate([[0], np.cumsum(caps[:-1], dtype=np.uint64)]).astype(np.uint64)
+    out = np.zeros(int(caps.sum()) + 64, np.uint8)
+    res = np.zeros(len(pkts), quic.RESULT_DTYPE)
+    ws = np.zeros(quic.workspace_size(len(pkts)), np.uint8)
+    quic.read_crypto_payload_batch(p(buf), p(off), p(lens), len(pkts), p(out), p(out_off), p(caps), p(res), p(ws),
+                                   stream=0)
+    qc.check_crypto(pkts, out, out_off, caps, res)
+    assert not out[int(caps.sum()):].any()
+
+
 if __name__ == "__main__":
     lib = _lib.load()
     which = sys.argv[1]
@@ -240,6 +269,8 @@ if __name__ == "__main__":
         case_ragged(args[0], args[1], args[2], bool(args[3]), ["packed", "slotted"][args[4]])
     elif which == "punch":
         case_punch(args[0], args[1], args[2])
+    elif which == "quic":
+        case_quic(args[0])
     elif which == "gecko":
         case_gecko(args[0], args[1])
     print("ok", which, args)

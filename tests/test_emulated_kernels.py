@@ -50,6 +50,7 @@ CASES = [
     ("far", "200 300 15 0", "8"),
     ("gecko", "40 7", "2"),              # Gecko frame encode + parse kernels (gecko.hip)
     ("punch", "300 5 3", "2"),           # realm punch matcher (realm.hip)
+    ("quic", "2", "2"),                  # QUIC Initial unprotect + ReadCryptoPayload kernels (quic.hip)
 ]
 
 
@@ -125,7 +126,7 @@ def test_emulated_wave_kernel_packed_run_lengths(emu_lib, which, args, run_log2)
 @pytest.mark.parametrize("which,args,cus", CASES)
 def test_emulated_persistent_kernel(emu_lib, which, args, cus):
     """The persistent workgroup kernel (HYOBFS_KERNEL=persistent) on the same cases."""
-    if which in ("conn", "host", "coalesce"):
+    if which in ("conn", "host", "coalesce", "quic"):
         pytest.skip("kernel-independent host paths run once, under the default kernel")
     _run(emu_lib, which, args, {"HYEMU_CUS": cus, "HYOBFS_KERNEL": "persistent"})
 
