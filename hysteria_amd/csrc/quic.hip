@@ -310,6 +310,23 @@ __device__ __forceinline__ uint32_t sub_word(const uint32_t* te, uint32_t w) {
            ((te[w >> 24] << 16) & 0xff000000u);
 }
 
+// round keys as little-endian column words, written to LDS as they are made
+// (a 4-word window in registers); called by one lane
+__device__ __forceinline__ void aes_expand_to(const uint32_t* te, const uint32_t k[4], uint32_t* dst) {
+    uint32_t w0 = k[0], w1 = k[1], w2 = k[2], w3 = k[3];
+    dst[0] = w0; dst[1] = w1; dst[2] = w2; dst[3] = w3;
+    uint32_t rcon = 1;
+#pragma unroll
+    for (int r = 1; r <= 10; ++r) {
+        w0 ^= sub_word(te, (w3 >> 8) | (w3 << 24)) ^ rcon;
+        w1 ^= w0;
+        w2 ^= w1;
+        w3 ^= w2;
+        rcon = ((rcon << 1) ^ ((rcon & 0x80) ? 0x1b : 0)) & 0xff;
+        dst[4 * r] = w0; dst[4 * r + 1] = w1; dst[4 * r + 2] = w2; dst[4 * r + 3] = w3;
+    }
+}
+
 // round keys as little-endian column words
 __device__ __forceinline__ void aes_expand(const uint32_t* te, const uint32_t k[4], uint32_t rk[44]) {
     rk[0] = k[0]; rk[1] = k[1]; rk[2] = k[2]; rk[3] = k[3];
@@ -325,7 +342,7 @@ __device__ __forceinline__ void aes_expand(const uint32_t* te, const uint32_t k[
     }
 }
 
-__device__ __forceinline__ void aes_encrypt(const uint32_t* te, const uint32_t rk[44], const uint32_t in[4],
+__device__ __forceinline__ void aes_encrypt(const uint32_t* te, const uint32_t* rk, const uint32_t in[4],
                                             uint32_t out[4]) {
     uint32_t s0 = in[0] ^ rk[0], s1 = in[1] ^ rk[1], s2 = in[2] ^ rk[2], s3 = in[3] ^ rk[3];
 #pragma unroll
@@ -354,24 +371,6 @@ struct G128 {
     uint64_t h, l;
 };
 
-QHD G128 gf_mul(G128 x, G128 y) {
-    G128 z{0, 0};
-    uint64_t vh = y.h, vl = y.l;
-    for (int half = 0; half < 2; ++half) {
-        const uint64_t xw = half ? x.l : x.h;
-#pragma unroll 8
-        for (int i = 63; i >= 0; --i) {
-            const uint64_t m = 0 - ((xw >> i) & 1);
-            z.h ^= vh & m;
-            z.l ^= vl & m;
-            const uint64_t lsb = 0 - (vl & 1);
-            vl = (vl >> 1) | (vh << 63);
-            vh = (vh >> 1) ^ (lsb & 0xE100000000000000ull);
-        }
-    }
-    return z;
-}
-
 QHD uint32_t bswap32(uint32_t x) {
     return (x >> 24) | ((x >> 8) & 0xff00) | ((x << 8) & 0xff0000) | (x << 24);
 }
@@ -379,6 +378,68 @@ QHD uint32_t bswap32(uint32_t x) {
 // 16 block bytes as 4 little-endian words -> G128
 QHD G128 g_from_le(const uint32_t w[4]) {
     return G128{(uint64_t)bswap32(w[0]) << 32 | bswap32(w[1]), (uint64_t)bswap32(w[2]) << 32 | bswap32(w[3])};
+}
+
+// times x: one right shift with the reduction x^128 = x^7 + x^2 + x + 1
+QHD G128 mulx(G128 v) {
+    const uint64_t lsb = 0 - (v.l & 1);
+    return G128{(v.h >> 1) ^ (lsb & 0xE100000000000000ull), (v.l >> 1) | (v.h << 63)};
+}
+
+// P^2: squaring is linear over GF(2): spread the bits of the natural-order
+// polynomial (bit i = x^i, the bit reversal of GCM's order), then fold the
+// upper 128 bits with x^128 = x^7 + x^2 + x + 1
+QHD uint64_t spread32(uint64_t x) {
+    x = (x | x << 16) & 0x0000FFFF0000FFFFull;
+    x = (x | x << 8) & 0x00FF00FF00FF00FFull;
+    x = (x | x << 4) & 0x0F0F0F0F0F0F0F0Full;
+    x = (x | x << 2) & 0x3333333333333333ull;
+    return (x | x << 1) & 0x5555555555555555ull;
+}
+
+QHD G128 gf_sqr(G128 v) {
+    const uint64_t n0 = __builtin_bitreverse64(v.h), n1 = __builtin_bitreverse64(v.l);
+    const uint64_t s0 = spread32(n0 & 0xffffffffu), s1 = spread32(n0 >> 32);
+    const uint64_t s2 = spread32(n1 & 0xffffffffu), s3 = spread32(n1 >> 32);
+    const uint64_t o = (s3 >> 63) ^ (s3 >> 62) ^ (s3 >> 57);   // degrees 128..134 of the shifted copies
+    const uint64_t r0 = s0 ^ s2 ^ (s2 << 1) ^ (s2 << 2) ^ (s2 << 7) ^ o ^ (o << 1) ^ (o << 2) ^ (o << 7);
+    const uint64_t r1 = s1 ^ s3 ^ (s3 << 1 | s2 >> 63) ^ (s3 << 2 | s2 >> 62) ^ (s3 << 7 | s2 >> 57);
+    return G128{__builtin_bitreverse64(r0), __builtin_bitreverse64(r1)};
+}
+
+// Shoup's 4-bit tables (a wave-uniform multiplier P): tab[i] = P * i(x), nibble
+// bit 3 = x^0 .. bit 0 = x^3 in GCM's reflected order; lanes 0..15 write one each.
+__device__ __forceinline__ void shoup_build(G128* tab, G128 P, uint32_t lane) {
+    if (lane < 16) {
+        const G128 p1 = mulx(P), p2 = mulx(p1), p3 = mulx(p2);
+        G128 e{0, 0};
+        if (lane & 8) { e.h ^= P.h; e.l ^= P.l; }
+        if (lane & 4) { e.h ^= p1.h; e.l ^= p1.l; }
+        if (lane & 2) { e.h ^= p2.h; e.l ^= p2.l; }
+        if (lane & 1) { e.h ^= p3.h; e.l ^= p3.l; }
+        tab[lane] = e;
+    }
+}
+
+// x * P through P's table: Horner over the 32 nibbles of x, last nibble first
+__device__ __forceinline__ G128 shoup_mul(G128 x, const G128* tab) {
+    G128 z{0, 0};
+#pragma unroll 4
+    for (int j = 31; j >= 0; --j) {
+        if (j != 31) {
+            // the 4 dropped bits times x^4: clmul(rem, 0x1C20) in the top 16 bits
+            const uint32_t rem = (uint32_t)z.l & 0xf;
+            const uint32_t red = ((rem & 1) * 0x1C20u) ^ ((rem & 2) * 0x1C20u) ^ ((rem & 4) * 0x1C20u) ^
+                                 ((rem & 8) * 0x1C20u);
+            z.l = (z.l >> 4) | (z.h << 60);
+            z.h = (z.h >> 4) ^ ((uint64_t)red << 48);
+        }
+        const uint32_t nib = j >= 16 ? (uint32_t)(x.l >> (4 * (31 - j))) & 0xf : (uint32_t)(x.h >> (4 * (15 - j))) & 0xf;
+        const G128 t = tab[nib];
+        z.h ^= t.h;
+        z.l ^= t.l;
+    }
+    return z;
 }
 
 // ------------------------------------------------------------------ ChaCha20 (RFC 8439 2.3)
@@ -593,16 +654,23 @@ struct Window {
     }
 };
 
+#ifndef HY_QUIC_MIN_WAVES
+#define HY_QUIC_MIN_WAVES 4   // waves per SIMD the open kernel is register-capped for
+#endif
+
 template <bool CRYPTO>
-__global__ __launch_bounds__(64) void quic_open_kernel(OpenArgs a) {
+__global__ __launch_bounds__(64, HY_QUIC_MIN_WAVES) void quic_open_kernel(OpenArgs a) {
     __shared__ uint32_t te[256];
+    __shared__ G128 gtab[7][16];   // GHASH: Shoup tables of H^(2^k)
+    __shared__ uint32_t rkl[44];   // AES-128 round keys of the packet's AEAD key
+    __shared__ uint32_t hrkl[44];  // ... and of its header-protection key
     __shared__ Frame fr[HYOBFS_QUIC_MAX_FRAMES];
     __shared__ uint16_t order[HYOBFS_QUIC_MAX_FRAMES];
     const uint32_t lane = threadIdx.x & 63;
     aes_table_load(te, lane);
-    __syncthreads();
 
     for (uint64_t pk = blockIdx.x; pk < a.n; pk += gridDim.x) {
+        __syncthreads();   // the previous packet's LDS reads are done
         uint8_t* p = a.packets + a.off[pk];
         hyobfs_quic_key key;
         int64_t pn_off, pn_max;
@@ -625,7 +693,7 @@ __global__ __launch_bounds__(64) void quic_open_kernel(OpenArgs a) {
         // UnProtect (packet_protector.go:46-79)
         if (st == HYOBFS_OK && (pn_off < 0 || (uint64_t)pn_off > L || L - (uint64_t)pn_off < 20))
             st = HYOBFS_QUIC_ERR_TOO_SMALL;
-        const bool aes = key.suite == HYOBFS_QUIC_TLS_AES_128_GCM_SHA256;
+        const bool aes = CRYPTO || key.suite == HYOBFS_QUIC_TLS_AES_128_GCM_SHA256;   // Initial packets: AES-128-GCM
         if (st == HYOBFS_OK && !aes && key.suite != HYOBFS_QUIC_TLS_CHACHA20_POLY1305_SHA256)
             st = HYOBFS_QUIC_ERR_SUITE;
         if (st != HYOBFS_OK) {
@@ -646,14 +714,17 @@ __global__ __launch_bounds__(64) void quic_open_kernel(OpenArgs a) {
         // header protection mask from the 16-byte sample at pnOffset + 4
         uint32_t sample[4], mw0, mw1;
         load_block(p, (uint64_t)pn_off + 4, L, sample);
-        uint32_t rk[44];
+        const uint32_t* rk = rkl;   // round keys live in LDS: registers stay free for occupancy
         if (aes) {
-            uint32_t hrk[44], m[4];
-            aes_expand(te, hpw, hrk);
-            aes_encrypt(te, hrk, sample, m);
+            uint32_t m[4];
+            if (lane == 0) {
+                aes_expand_to(te, hpw, hrkl);
+                aes_expand_to(te, kw, rkl);
+            }
+            __syncthreads();
+            aes_encrypt(te, hrkl, sample, m);
             mw0 = m[0];
             mw1 = m[1];
-            aes_expand(te, kw, rk);
         } else {
             uint32_t ks[16];
             chacha20_block(hpw, sample[0], sample + 1, ks);
@@ -711,32 +782,39 @@ __global__ __launch_bounds__(64) void quic_open_kernel(OpenArgs a) {
         uint32_t tagw[4];
         if (ok) load_block(p, L - 16, L, tagw);
         if (ok && aes) {
-            // H = E(K, 0), GHASH split over lanes: lane l holds sum_t X_{m-1-l-64t} H^(64t)
+            // H = E(K, 0) and Shoup tables of H^(2^k), k = 0..6
             const uint32_t zero[4] = {0, 0, 0, 0};
             uint32_t hw[4];
             aes_encrypt(te, rk, zero, hw);
-            const G128 H = g_from_le(hw);
-            G128 hp2[7];
-            hp2[0] = H;
-#pragma unroll
-            for (int k = 1; k < 7; ++k) hp2[k] = gf_mul(hp2[k - 1], hp2[k - 1]);   // H^(2^k)
+            G128 P = g_from_le(hw);
+            shoup_build(gtab[0], P, lane);
+            for (int k = 1; k < 7; ++k) {
+                P = gf_sqr(P);
+                shoup_build(gtab[k], P, lane);
+            }
+            __syncthreads();
+            // lane l: acc_l = sum_t X_{m-1-l-64t} H^(64t), Horner in the uniform H^64
             G128 acc{0, 0};
             for (uint64_t t = nt; t-- > 0;) {
                 uint32_t w[4];
                 stream_block(m - 1 - lane - 64 * t, w, false);
                 const G128 x = g_from_le(w);
-                acc = gf_mul(acc, hp2[6]);
+                if (t + 1 != nt) acc = shoup_mul(acc, gtab[6]);
                 acc.h ^= x.h;
                 acc.l ^= x.l;
             }
-            G128 pw{0x8000000000000000ull, 0};   // the field's 1
-            const uint32_t e = lane + 1;
+            // lane tree: sum_l acc_l H^l, one multiply by the uniform H^(2^k) per level;
+            // then times H, so block s carries H^(m-s)
 #pragma unroll
-            for (int k = 0; k < 7; ++k)
-                if ((e >> k) & 1) pw = gf_mul(pw, hp2[k]);
-            acc = nt ? gf_mul(acc, pw) : G128{0, 0};
-            acc.h = wave_xor(acc.h);
-            acc.l = wave_xor(acc.l);
+            for (int k = 0; k < 6; ++k) {
+                const int src = (int)((lane + (1u << k)) & 63);
+                G128 b{__shfl(acc.h, src, 64), __shfl(acc.l, src, 64)};
+                b = shoup_mul(b, gtab[k]);
+                acc.h ^= b.h;
+                acc.l ^= b.l;
+            }
+            acc = G128{__shfl(acc.h, 0, 64), __shfl(acc.l, 0, 64)};
+            acc = shoup_mul(acc, gtab[0]);
             // tag = E(K, J0) ^ S
             const uint32_t j0[4] = {nonce[0], nonce[1], nonce[2], 0x01000000u};
             uint32_t ej[4];

@@ -12,7 +12,7 @@ for m in $MODE; do
     test) step pytest 700 python -u -m pytest tests -x -v -m gpu --timeout 120 --timeout-method thread > $O/pytest_gpu.log 2>&1 ;;
     quic) step pytest_quic 300 python -u -m pytest tests/test_gpu_quic.py -x -v -m gpu --timeout 120 --timeout-method thread > $O/pytest_quic.log 2>&1 ;;
     qbench) step bench_quic 300 python -u scripts/bench_quic.py > $O/bench_quic.json 2> $O/bench_quic.err ;;
-    qprof) step qprof 300 rocprofv3 --kernel-trace --stats -d $O/qprof -o run -- python scripts/bench_quic.py --steps 10 > $O/qprof.log 2>&1 ;;
+    qprof) step qprof 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/qprof -o run -- python scripts/bench_quic.py --steps 10 > $O/qprof.log 2>&1 ;;
     bench) step bench 300 python bench.py > $O/bench.json 2> $O/bench.err ;;
     prof) step collect 900 bash scripts/collect_profiles.sh r02 > $O/collect.log 2>&1 ;;
     udp)
