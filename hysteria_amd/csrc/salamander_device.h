@@ -421,7 +421,10 @@ __device__ __forceinline__ void store_masked(uint8_t* dst, u128 r, uint32_t cov)
     }
 }
 
-constexpr int kU = 4;   // chunks per lane per sweep iteration
+#ifndef HY_KU
+#define HY_KU 4
+#endif
+constexpr int kU = HY_KU;   // chunks per lane per sweep iteration
 
 
 
