@@ -53,8 +53,159 @@ struct GeckoGroup {             // one wave's 64 frames, in LDS
     uint64_t hdr[64];           // the 5 header bytes, little-endian in the low bytes
     uint32_t wstart[65];        // first plaintext window of the frame (exclusive scan), [64] = total
     uint32_t hp_plain[64];      // chunk start (low 16 bits) | plaintext length (high 16 bits)
-    gk_u128 key[128];           // the frame's key, two halves
+    uint32_t rs[65];            // aligned path: wire start relative to the group base, [64] = end of all
+    uint64_t salt[64];          // aligned path: the salts (merged into the edge chunks)
+    gk_u128 key[128];           // the frame's key, two halves (aligned path: rotated to the wire phase)
 };
+
+// Pad stream bytes at plaintext [p0, p0 + 16) of frame f (p0 may be negative:
+// those bytes are garbage, masked by the caller): stream byte f*2048 + q is
+// byte q%8 of SplitMix64 output (f*2048 + q) / 8.
+__device__ __forceinline__ gk_u128 gk_pad_at(uint64_t seed, uint64_t f, int32_t p0) {
+    const int64_t sidx = (int64_t)(f * HYOBFS_GECKO_BUFFER_SIZE) + p0;
+    const uint64_t w = (uint64_t)(sidx >> 3);
+    const uint32_t sh = (uint32_t)(sidx & 7) * 8;
+    const uint64_t z = seed + (w + 1) * 0x9e3779b97f4a7c15ull;
+    const uint64_t w0 = gk_mix64(z), w1 = gk_mix64(z + 0x9e3779b97f4a7c15ull),
+                   w2 = gk_mix64(z + 2 * 0x9e3779b97f4a7c15ull);
+    const gk_u128 lo = (gk_u128)w1 << 64 | w0;
+    return sh ? (lo >> sh) | ((gk_u128)w2 << (128 - sh)) : lo;
+}
+
+#ifndef HY_GK_FORCE_WINDOWS
+#define HY_GK_FORCE_WINDOWS 0   // A/B and tests: 1 = always the plaintext-window path
+#endif
+
+// Frame k's bytes in the 16-byte wire chunk at rel (group-relative, 16-aligned)
+// address a: salt, then header / padding / chunk XOR the frame's key.
+__device__ __forceinline__ void gk_contrib(const hyobfs_gecko_batch& B, const GeckoGroup& G, uint64_t f0, uint32_t k,
+                                           uint32_t a, gk_u128& r, uint32_t& cov) {
+    const uint32_t hpl = G.hp_plain[k];
+    if (!hpl) return;
+    const int32_t hp = (int32_t)(hpl & 0xffff), plain = (int32_t)(hpl >> 16);
+    const uint32_t rs = G.rs[k];
+    const int32_t p0 = (int32_t)a - (int32_t)rs - HYOBFS_SALT_LEN;   // plaintext index of chunk byte 0
+    const int32_t xlo = max(p0, 0), xhi = min(p0 + 16, plain);
+    if (xlo < xhi) {
+        gk_u128 X = 0;
+        const int32_t hhi = min(p0 + 16, (int32_t)HYOBFS_GECKO_HEADER_LEN);
+        if (xlo < hhi) {   // header
+            const gk_u128 H = (gk_u128)G.hdr[k];
+            X |= (p0 <= 0 ? H << (8 * -p0) : H >> (8 * p0)) & gk_mask(xlo - p0, hhi - p0);
+        }
+        const int32_t plo = max(p0, (int32_t)HYOBFS_GECKO_HEADER_LEN), phi = min(p0 + 16, hp);
+        if (plo < phi) X |= gk_pad_at(B.pad_seed, f0 + k, p0) & gk_mask(plo - p0, phi - p0);
+        const int32_t clo = max(p0, hp);
+        if (clo < xhi) {   // chunk bytes
+            const uint8_t* __restrict__ ch = B.msg + G.chunk_off[k];
+            const int32_t clen = plain - hp, cb = p0 - hp;
+            gk_u128 Xc = 0;
+            if (clen >= 16) {   // one in-bounds 16-byte load, shifted into place
+                const int32_t ws = min(max(cb, 0), clen - 16), d = ws - cb;
+                const gk_u128 V = gk_load16u(ch + ws);
+                Xc = d >= 0 ? V << (8 * d) : V >> (8 * -d);
+            } else {
+                for (int32_t j = clo; j < xhi; ++j) Xc |= (gk_u128)ch[j - hp] << (8 * (j - p0));
+            }
+            X |= Xc & gk_mask(clo - p0, xhi - p0);
+        }
+        r |= (X ^ G.key[2 * k + ((a >> 4) & 1)]) & gk_mask(xlo - p0, xhi - p0);
+        cov |= ((1u << (xhi - xlo)) - 1u) << (xlo - p0);
+    }
+    const uint32_t slo = max(rs, a), shi = min(rs + HYOBFS_SALT_LEN, a + 16);
+    if (slo < shi) {   // salt
+        const gk_u128 S = (gk_u128)G.salt[k];
+        r |= (rs >= a ? S << (8 * (rs - a)) : S >> (8 * (a - rs))) & gk_mask(slo - a, shi - a);
+        cov |= ((1u << (shi - slo)) - 1u) << (slo - a);
+    }
+}
+
+// The aligned sweep of one wave's group (see the kernel comment).
+__device__ __forceinline__ void gecko_encode_aligned(const KeyParams& K, const hyobfs_gecko_batch& B, GeckoGroup& G,
+                                                  uint64_t f0, uint32_t lane, bool valid, uint64_t oo,
+                                                  uint64_t prevE, uint64_t maxE, unsigned long long vmask,
+                                                  uint32_t plain, uint64_t salt, gk_u128 k0, gk_u128 k1) {
+    (void)K;
+    const uint64_t base = uni64(__shfl(oo, (int)__builtin_ctzll(vmask), 64)) & ~15ull;
+    const uint32_t rs = valid ? (uint32_t)(oo - base) : (prevE > base ? (uint32_t)(prevE - base) : 0u);
+    const uint32_t rend = (uint32_t)(maxE - base);
+    G.rs[lane] = rs;
+    if (lane == 0) G.rs[64] = rend;
+    if (!valid) G.hp_plain[lane] = 0;
+    if (valid) {   // the key rotated so that rel address (a + b) mod 32 indexes it
+        const uint64_t kw[4] = {(uint64_t)k0, (uint64_t)(k0 >> 64), (uint64_t)k1, (uint64_t)(k1 >> 64)};
+        uint64_t kr[4];
+        rotl_key_bytes(kw, (rs + HYOBFS_SALT_LEN) & 31u, kr);
+        G.key[2 * lane] = (gk_u128)kr[1] << 64 | kr[0];
+        G.key[2 * lane + 1] = (gk_u128)kr[3] << 64 | kr[2];
+        G.salt[lane] = salt;
+    }
+    hy_wave_sync();
+    uint8_t* __restrict__ ob = B.out + base;
+    const uint32_t tc = (rend + 15) >> 4;   // chunks of the group's wire range
+    // a chunk is interior when it lies inside one frame's padding or chunk bytes
+    auto interior = [&](uint32_t q, uint32_t a, int32_t& p, int32_t& hp) {
+        const uint32_t hpl = G.hp_plain[q];
+        hp = (int32_t)(hpl & 0xffff);
+        const int32_t pl = (int32_t)(hpl >> 16);
+        p = (int32_t)a - (int32_t)G.rs[q] - HYOBFS_SALT_LEN;
+        return hpl != 0 && ((p >= (int32_t)HYOBFS_GECKO_HEADER_LEN && p + 16 <= hp) || (p >= hp && p + 16 <= pl));
+    };
+    // ---- sweep: lane windows move forward by 64 chunks, so the frame walk does too
+    uint32_t q = 0;
+    for (uint32_t T = 0; T < tc; T += 64 * kGkU) {
+        gk_u128 v[kGkU];
+        bool ok[kGkU];
+#pragma unroll
+        for (int u = 0; u < kGkU; ++u) {
+            const uint32_t c = T + lane + 64 * u, a = 16 * c;
+            v[u] = 0;
+            ok[u] = false;
+            if (c < tc) {
+                while (G.rs[q + 1] <= a) ++q;   // rs[64] = the range end > a stops it
+                int32_t p, hp;
+                ok[u] = interior(q, a, p, hp);
+                if (ok[u]) {
+                    v[u] = p >= hp ? gk_load16u(B.msg + G.chunk_off[q] + (p - hp)) : gk_pad_at(B.pad_seed, f0 + q, p);
+                    v[u] ^= G.key[2 * q + ((a >> 4) & 1)];
+                }
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < kGkU; ++u)
+            if (ok[u]) store16_stream(ob + 16 * (T + lane + 64 * u), v[u]);
+    }
+    // ---- edge chunks of frame `lane`: the first two (salt, header), the one holding
+    // the padding/chunk seam, the last; a chunk an earlier frame reaches into is that
+    // frame's, and its owner merges every frame that touches it
+    if (valid) {
+        const uint32_t hp = G.hp_plain[lane] & 0xffff;
+        const uint32_t cs = rs >> 4, ce = (rs + HYOBFS_SALT_LEN + plain - 1) >> 4;
+        const uint32_t seam = (rs + HYOBFS_SALT_LEN + hp - 1) >> 4;
+        const uint32_t prel = prevE > base ? (uint32_t)(prevE - base) : 0u;
+        auto cand = [&](int i) { return i == 0 ? cs : i == 1 ? cs + 1 : i == 2 ? seam : ce; };
+        uint32_t m = 0;   // distinct candidates this lane owns
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            bool dup = cand(i) > ce || (i == 0 && prel > 16 * cs);
+#pragma unroll
+            for (int d = 0; d < i; ++d) dup = dup || cand(d) == cand(i);
+            if (!dup) m |= 1u << i;
+        }
+#pragma unroll 1
+        while (m) {
+            const uint32_t c = cand(__builtin_ctz(m)), a = 16 * c;
+            m &= m - 1;
+            int32_t p, php;
+            if (interior(lane, a, p, php)) continue;
+            gk_u128 r = 0;
+            uint32_t cov = 0;
+            for (uint32_t k = lane; k < 64 && G.rs[k] < a + 16; ++k) gk_contrib(B, G, f0, k, a, r, cov);
+            if (cov == 0xFFFFu) store16_stream(ob + a, r);
+            else if (cov) store_masked(ob + a, r, cov);
+        }
+    }
+}
 
 #ifdef HY_GK_WPE   // A/B builds only: register cap for the fused hash
 #define HY_GK_ATTR __attribute__((amdgpu_waves_per_eu(HY_GK_WPE)))
@@ -70,38 +221,64 @@ __global__ __launch_bounds__(256) HY_GK_ATTR void gecko_encode_kernel(KeyParams 
     if (f0 >= B.n) return;
     // ---- 1. lane l: frame f0 + l's record, offsets, salt and key into LDS
     const uint64_t f = f0 + lane;
-    uint32_t nwin = 0;
+    uint32_t nwin = 0, plain = 0;
+    uint64_t oo = 0, salt = 0;
+    gk_u128 k0 = 0, k1 = 0;
     if (f < B.n) {
         const hyobfs_gecko_frame fr = B.frames[f];
         const uint32_t total = fr.idx_total & 0x0f, idx = fr.idx_total >> 4;
         const uint32_t hp = HYOBFS_GECKO_HEADER_LEN + fr.pad_len;
         const uint64_t plain64 = (uint64_t)hp + fr.chunk_len;   // 64-bit: a hostile chunk_len must not wrap
-        const uint32_t plain = (uint32_t)plain64;
         if (total >= HYOBFS_GECKO_MIN_CHUNKS && total <= HYOBFS_GECKO_MAX_CHUNKS && idx < total &&
             HYOBFS_SALT_LEN + plain64 <= HYOBFS_GECKO_BUFFER_SIZE) {   // else: skipped, nothing written
+            plain = (uint32_t)plain64;
             nwin = (plain + 15) >> 4;
-            const uint64_t oo = B.out_off[f];
+            oo = B.out_off[f];
             G.out_off[lane] = oo;
             G.chunk_off[lane] = fr.chunk_off;
             G.hdr[lane] = (uint64_t)HYOBFS_GECKO_FLAG_FRAGMENT | (uint64_t)fr.msg_id << 8 |
                           (uint64_t)fr.idx_total << 16 | (uint64_t)(fr.pad_len >> 8) << 24 |
                           (uint64_t)(fr.pad_len & 0xff) << 32;
             G.hp_plain[lane] = hp | plain << 16;
-            const uint64_t salt = B.salts[f];
+            salt = B.salts[f];
 #ifdef HY_GK_KEYS_KERNEL   // A/B builds only: keys from keys_kernel via the workspace
             const uint8_t* kp = static_cast<const uint8_t*>(B.workspace) + 32 * f;
-            gk_u128 k0, k1;
             __builtin_memcpy(&k0, kp, 16);
             __builtin_memcpy(&k1, kp + 16, 16);
 #else   // keyLocked (salamander.go:88-91) in registers; the hash overlaps other waves' sweeps
             uint64_t kw[4];
             salamander_key(K, salt, kw);
-            const gk_u128 k0 = (gk_u128)kw[1] << 64 | kw[0], k1 = (gk_u128)kw[3] << 64 | kw[2];
+            k0 = (gk_u128)kw[1] << 64 | kw[0];
+            k1 = (gk_u128)kw[3] << 64 | kw[2];
 #endif
-            G.key[2 * lane] = k0;
-            G.key[2 * lane + 1] = k1;
-            __builtin_memcpy(B.out + oo, &salt, HYOBFS_SALT_LEN);
         }
+    }
+    // Aligned path when the group's valid frames are in ascending, non-overlapping
+    // wire order (what plan_fragments / writeFragmented produce): sweep the
+    // group's wire range in aligned 16-byte chunks, so every interior line leaves
+    // whole; otherwise the plaintext-window path below.
+    const bool valid = nwin != 0;
+    const uint64_t wend = oo + HYOBFS_SALT_LEN + plain;
+    uint64_t incE = valid ? wend : 0;   // inclusive max-scan of wire ends
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint64_t y = __shfl_up(incE, d, 64);
+        if (lane >= (uint32_t)d) incE = max(incE, y);
+    }
+    uint64_t prevE = __shfl_up(incE, 1, 64);
+    if (lane == 0) prevE = 0;
+    const uint64_t maxE = uni64(__shfl(incE, 63, 64));
+    const unsigned long long vmask = __ballot(valid);
+    const bool aligned = !HY_GK_FORCE_WINDOWS && vmask != 0 && !__ballot(valid && oo < prevE) &&
+                         maxE - (uni64(__shfl(oo, (int)__builtin_ctzll(vmask), 64)) & ~15ull) < (1ull << 31);
+    if (aligned) {
+        gecko_encode_aligned(K, B, G, f0, lane, valid, oo, prevE, maxE, vmask, plain, salt, k0, k1);
+        return;
+    }
+    if (valid) {
+        G.key[2 * lane] = k0;
+        G.key[2 * lane + 1] = k1;
+        __builtin_memcpy(B.out + oo, &salt, HYOBFS_SALT_LEN);
     }
     uint32_t inc = nwin;   // inclusive scan of window counts
 #pragma unroll

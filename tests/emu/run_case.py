@@ -148,8 +148,11 @@ def case_host(n, L, chunk, obf):
         assert out[i * out_stride:i * out_stride + len(exp)].tobytes() == exp, i
 
 
-def case_gecko(n_msgs, seed):
-    """Gecko frames: one device encode pass vs oracle/gecko_ref, then deobfuscate + parse."""
+def case_gecko(n_msgs, seed, layout=0):
+    """Gecko frames: one device encode pass vs oracle/gecko_ref, then deobfuscate + parse.
+    layout 0: packed wire order (the aligned sweep); 1: ascending with gaps between
+    frames (aligned sweep, gap bytes untouched); 2: frames placed in shuffled order
+    (the plaintext-window path)."""
     from hysteria_amd import gecko
     from oracle import gecko_ref as gref
     psk = b"average_password"
@@ -159,6 +162,16 @@ def case_gecko(n_msgs, seed):
     msg = rng.integers(0, 256, int(lens.sum()) + 16, dtype=np.uint8)
     fr, off, total = gecko.plan_fragments(lens, 400, 900, first_msg_id=seed)
     nf = len(fr)
+    if layout:
+        widths = np.diff(np.append(off, total)).astype(np.uint64)
+        order = rng.permutation(nf) if layout == 2 else np.arange(nf)
+        gaps = rng.integers(0, 41, nf).astype(np.uint64) if layout == 1 else np.zeros(nf, np.uint64)
+        pos = np.zeros(nf, np.uint64)
+        cur = np.uint64(3)
+        for i in order:
+            pos[i] = cur
+            cur += widths[i] + gaps[i]
+        off, total = pos, int(cur)
     salts = ref.splitmix64_array(5, 0, nf)
     out = np.full(total + 64, 0xA5, np.uint8)
     ws = np.zeros(gecko.workspace_size(nf), np.uint8)
@@ -168,8 +181,11 @@ def case_gecko(n_msgs, seed):
                        workspace=p(ws), n=nf, stream=0)
     exp = gref.encode_wire(psk, msg.tobytes(), fr.tolist(), salts, 99)
     assert out[total:].tobytes() == b"\xa5" * 64
+    written = np.zeros(total + 64, bool)
     for i in range(nf):
         assert out[int(off[i]):int(off[i]) + len(exp[i])].tobytes() == exp[i], i
+        written[int(off[i]):int(off[i]) + len(exp[i])] = True
+    assert (out[~written] == 0xA5).all(), "wrote outside the frames"
     # back: Salamander deobfuscate batch, then the Gecko parse kernel
     wl = np.array([len(e) for e in exp], np.uint32)
     plain = np.zeros(total, np.uint8)
@@ -272,6 +288,6 @@ if __name__ == "__main__":
     elif which == "quic":
         case_quic(args[0])
     elif which == "gecko":
-        case_gecko(args[0], args[1])
+        case_gecko(*args)
     print("ok", which, args)
 

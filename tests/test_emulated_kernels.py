@@ -48,7 +48,9 @@ CASES = [
     ("coalesce", "8 150 4 32", "2"),     # many threads on one coalescing conn (hyobfs_conn_set_coalescing)
     ("far", "200 300 15 1", "8"),        # workgroup bases beyond 2^31
     ("far", "200 300 15 0", "8"),
-    ("gecko", "40 7", "2"),              # Gecko frame encode + parse kernels (gecko.hip)
+    ("gecko", "40 7", "2"),              # Gecko frame encode + parse kernels (gecko.hip), aligned sweep
+    ("gecko", "60 8 1", "2"),            # ... ascending frames with gaps: gap bytes untouched
+    ("gecko", "60 9 2", "2"),            # ... shuffled placement: the plaintext-window path
     ("punch", "300 5 3", "2"),           # realm punch matcher (realm.hip)
     ("quic", "2", "2"),                  # QUIC Initial unprotect + ReadCryptoPayload kernels (quic.hip)
 ]
