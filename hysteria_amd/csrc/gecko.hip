@@ -126,7 +126,8 @@ __device__ __forceinline__ void gecko_encode_aligned(const KeyParams& K, const h
                                                   uint64_t prevE, uint64_t maxE, unsigned long long vmask,
                                                   uint32_t plain, uint64_t salt, gk_u128 k0, gk_u128 k1) {
     (void)K;
-    const uint64_t base = uni64(__shfl(oo, (int)__builtin_ctzll(vmask), 64)) & ~15ull;
+    // 256-aligned: each wave store instruction (64 lanes x 16 B) covers whole 128-B lines
+    const uint64_t base = uni64(__shfl(oo, (int)__builtin_ctzll(vmask), 64)) & ~255ull;
     const uint32_t rs = valid ? (uint32_t)(oo - base) : (prevE > base ? (uint32_t)(prevE - base) : 0u);
     const uint32_t rend = (uint32_t)(maxE - base);
     G.rs[lane] = rs;
@@ -151,31 +152,8 @@ __device__ __forceinline__ void gecko_encode_aligned(const KeyParams& K, const h
         p = (int32_t)a - (int32_t)G.rs[q] - HYOBFS_SALT_LEN;
         return hpl != 0 && ((p >= (int32_t)HYOBFS_GECKO_HEADER_LEN && p + 16 <= hp) || (p >= hp && p + 16 <= pl));
     };
-    // ---- sweep: lane windows move forward by 64 chunks, so the frame walk does too
-    uint32_t q = 0;
-    for (uint32_t T = 0; T < tc; T += 64 * kGkU) {
-        gk_u128 v[kGkU];
-        bool ok[kGkU];
-#pragma unroll
-        for (int u = 0; u < kGkU; ++u) {
-            const uint32_t c = T + lane + 64 * u, a = 16 * c;
-            v[u] = 0;
-            ok[u] = false;
-            if (c < tc) {
-                while (G.rs[q + 1] <= a) ++q;   // rs[64] = the range end > a stops it
-                int32_t p, hp;
-                ok[u] = interior(q, a, p, hp);
-                if (ok[u]) {
-                    v[u] = p >= hp ? gk_load16u(B.msg + G.chunk_off[q] + (p - hp)) : gk_pad_at(B.pad_seed, f0 + q, p);
-                    v[u] ^= G.key[2 * q + ((a >> 4) & 1)];
-                }
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < kGkU; ++u)
-            if (ok[u]) store16_stream(ob + 16 * (T + lane + 64 * u), v[u]);
-    }
-    // ---- edge chunks of frame `lane`: the first two (salt, header), the one holding
+    // ---- first, the edge chunks of frame `lane` (plain stores, so each such line is
+    // still in the L2 when the sweep's streaming stores complete it): the first two (salt, header), the one holding
     // the padding/chunk seam, the last; a chunk an earlier frame reaches into is that
     // frame's, and its owner merges every frame that touches it
     if (valid) {
@@ -201,9 +179,33 @@ __device__ __forceinline__ void gecko_encode_aligned(const KeyParams& K, const h
             gk_u128 r = 0;
             uint32_t cov = 0;
             for (uint32_t k = lane; k < 64 && G.rs[k] < a + 16; ++k) gk_contrib(B, G, f0, k, a, r, cov);
-            if (cov == 0xFFFFu) store16_stream(ob + a, r);
+            if (cov == 0xFFFFu) gk_store16u(ob + a, r);   // a plain store: the line stays in L2 for the sweep's part
             else if (cov) store_masked(ob + a, r, cov);
         }
+    }
+    // ---- sweep: lane windows move forward by 64 chunks, so the frame walk does too
+    uint32_t q = 0;
+    for (uint32_t T = 0; T < tc; T += 64 * kGkU) {
+        gk_u128 v[kGkU];
+        bool ok[kGkU];
+#pragma unroll
+        for (int u = 0; u < kGkU; ++u) {
+            const uint32_t c = T + lane + 64 * u, a = 16 * c;
+            v[u] = 0;
+            ok[u] = false;
+            if (c < tc) {
+                while (G.rs[q + 1] <= a) ++q;   // rs[64] = the range end > a stops it
+                int32_t p, hp;
+                ok[u] = interior(q, a, p, hp);
+                if (ok[u]) {
+                    v[u] = p >= hp ? gk_load16u(B.msg + G.chunk_off[q] + (p - hp)) : gk_pad_at(B.pad_seed, f0 + q, p);
+                    v[u] ^= G.key[2 * q + ((a >> 4) & 1)];
+                }
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < kGkU; ++u)
+            if (ok[u]) store16_stream(ob + 16 * (T + lane + 64 * u), v[u]);
     }
 }
 
@@ -270,7 +272,7 @@ __global__ __launch_bounds__(256) HY_GK_ATTR void gecko_encode_kernel(KeyParams 
     const uint64_t maxE = uni64(__shfl(incE, 63, 64));
     const unsigned long long vmask = __ballot(valid);
     const bool aligned = !HY_GK_FORCE_WINDOWS && vmask != 0 && !__ballot(valid && oo < prevE) &&
-                         maxE - (uni64(__shfl(oo, (int)__builtin_ctzll(vmask), 64)) & ~15ull) < (1ull << 31);
+                         maxE - (uni64(__shfl(oo, (int)__builtin_ctzll(vmask), 64)) & ~255ull) < (1ull << 31);
     if (aligned) {
         gecko_encode_aligned(K, B, G, f0, lane, valid, oo, prevE, maxE, vmask, plain, salt, k0, k1);
         return;
