@@ -478,3 +478,28 @@ def assemble_crypto_frames(frames):   # payload.go:118-148
     for off, d in frames:
         out[off:off + len(d)] = d
     return bytes(out)
+
+
+# ------------------------------------------------------------------ C restatement (oracle/quic_ref.c)
+class CQuicOracle:
+    """ctypes view of oracle/libquic_ref.so: ReadCryptoPayload over a batch on
+    host threads (the CPU baseline of scripts/bench_quic.py)."""
+
+    def __init__(self, path: str | None = None):
+        import ctypes
+        import os
+        path = path or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libquic_ref.so")
+        self.lib = ctypes.CDLL(path)
+        vp, u64, u32, i32 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int
+        self.lib.quic_read_crypto_payload_batch.argtypes = [vp, vp, vp, u64, vp, u32, vp, vp, i32]
+        self.lib.quic_read_crypto_payload_batch.restype = i32
+
+    def read_batch(self, buf, off, lens, n: int, cap: int, threads: int = 1):
+        """(status int32[n], out_len uint32[n], out uint8[n*cap])."""
+        import numpy as np
+        out = np.zeros(n * cap, np.uint8)
+        st = np.zeros(n, np.int32)
+        ol = np.zeros(n, np.uint32)
+        self.lib.quic_read_crypto_payload_batch(buf.ctypes.data, off.ctypes.data, lens.ctypes.data, n,
+                                                out.ctypes.data, cap, st.ctypes.data, ol.ctypes.data, threads)
+        return st, ol, out

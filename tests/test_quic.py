@@ -133,3 +133,21 @@ def test_abi_result_and_key_layouts():
     key = ref.ProtectionKey(ref.TLS_AES_128_GCM_SHA256, bytes(range(32)), ref.V1)
     rec = np.frombuffer(qc.key_record(key), quic.KEY_DTYPE)[0]
     assert int(rec["suite"]) == 0x1301 and bytes(rec["iv"]) == key.iv and bytes(rec["key"][:16]) == key.key
+
+
+def test_c_oracle_matches_python_oracle():
+    """oracle/quic_ref.c (the CPU baseline) against oracle/quic_ref.py on every
+    ReadCryptoPayload case, on 3 host threads."""
+    import os
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    subprocess.run(["make", "-s", "-C", os.path.join(root, "oracle")], check=True)
+    co = ref.CQuicOracle()
+    pkts = qc.crypto_packets(1) + qc.crypto_packets(6)
+    buf, off, lens = qc.pack([p for _, p in pkts])
+    st, ol, out = co.read_batch(buf, off, lens, len(pkts), 4096, threads=3)
+    for i, (name, p) in enumerate(pkts):
+        s, d = qc.oracle_read(p)
+        assert int(st[i]) == s, name
+        if s == 0:
+            assert out[i * 4096:i * 4096 + int(ol[i])].tobytes() == d, name
