@@ -312,14 +312,24 @@ __global__ __launch_bounds__(kGroup* kWavesPerBlock, HY_WAVE_MIN_WAVES) void sal
     }
     if (!OBF && W) salt = load8u(in + ioff);   // the wire's salt
 
-    // ---- virtual layout: the wave's runs back to back, each from its
-    // 16-aligned real base; real address = virtual + delta (a multiple of 16)
+    // ---- virtual layout: the wave's runs one after another, each from its
+    // 16-aligned real base; real address = virtual + delta.  Each run starts at
+    // the virtual offset that makes delta a multiple of 128 (up to 7 unused
+    // chunks in front of it), so every 1 KiB store instruction of the sweep
+    // covers whole 128-byte lines of the output.
     const uint64_t rb = rfirst & ~15ull;
     uint64_t rend = W ? ooff + W : rb;   // end of the run's written bytes
     for (uint32_t m = 1; m < RUN; m <<= 1) rend = max(rend, (uint64_t)__shfl_xor(rend, (int)m, 64));
     const uint32_t nch = live ? (uint32_t)((rend - rb + 15) >> 4) : 0u;   // the run's chunks
-    const uint32_t vp = (uint32_t)wave_incl_scan(i == 0 ? nch : 0u, lane) - (i == 0 ? nch : 0u);
-    const uint32_t vrun = __shfl(vp, (int)(lane & ~(RUN - 1)), 64) << 4;   // run's virtual start
+#ifndef HY_LINE_ALIGN
+#define HY_LINE_ALIGN 1
+#endif
+    const uint32_t ph = HY_LINE_ALIGN ? (uint32_t)(rb >> 4) & 7u : 0u;   // the run base's chunk within its line
+    const uint32_t slots = HY_LINE_ALIGN ? (ph + nch + 7u) >> 3 : nch;   // virtual lines (or chunks) the run takes
+    const uint32_t vp = (uint32_t)wave_incl_scan(i == 0 ? slots : 0u, lane) - (i == 0 ? slots : 0u);
+    const uint32_t vrun = (HY_LINE_ALIGN ? (__shfl(vp, (int)(lane & ~(RUN - 1)), 64) << 3) + ph
+                                         : __shfl(vp, (int)(lane & ~(RUN - 1)), 64))
+                          << 4;   // run's virtual start
     const uint32_t rel = live ? vrun + (uint32_t)min<uint64_t>(ooff - rb, (uint64_t)nch << 4) : 0xFFFFFFFFu;
     const uint32_t end = W ? rel + W : 0u;
     uint32_t incm = end;   // inclusive max-scan of region ends (chunk ownership)
