@@ -46,6 +46,7 @@ struct hyobfs_salamander {
         hipStream_t s = nullptr;
         void* p = nullptr;
         uint64_t cap = 0;
+        hyobfs::SideLane side;   // HYOBFS_KERNEL_PIPE: key-pass stream + events, made on first use
     };
     std::vector<StreamWs> ws;
     std::mutex ws_mu;
@@ -235,14 +236,17 @@ size_t run_one(hyobfs_salamander* c, bool obf, const uint8_t* in, size_t in_len,
 }
 
 // The context's scratch for stream s, grown to `need` bytes.  Caller holds c->ws_mu.
-void* stream_workspace(hyobfs_salamander* c, hipStream_t s, uint64_t need) {
+void* stream_workspace(hyobfs_salamander* c, hipStream_t s, uint64_t need,
+                       hyobfs_salamander::StreamWs** entry = nullptr) {
     hyobfs_salamander::StreamWs* e = nullptr;
     for (auto& x : c->ws)
         if (x.s == s) e = &x;
     if (!e) {
-        c->ws.push_back({s, nullptr, 0});
+        c->ws.push_back(hyobfs_salamander::StreamWs{});
         e = &c->ws.back();
+        e->s = s;
     }
+    if (entry) *entry = e;
     if (e->cap < need) {
         if (e->p) {
             // only launches on s use this buffer, and every one of them was
@@ -299,7 +303,8 @@ inline uint64_t ctx_ws_bytes(const hyobfs_salamander* c, const hyobfs_batch* b, 
     uint64_t need = 0;
     if (b->n && b->out_stride == 0 && !b->workspace) need = (hyobfs_batch_workspace_size(b->n) + 255) & ~255ull;
     keys_off = need;
-    if (b->n >= 2 && hyobfs::resolve_kernel(c->kernel) == HYOBFS_KERNEL_STREAM) need += 32 * b->n;
+    const int kc = hyobfs::resolve_kernel(c->kernel);
+    if (b->n >= 2 && (kc == HYOBFS_KERNEL_STREAM || kc == HYOBFS_KERNEL_PIPE)) need += 32 * b->n;
     return need;
 }
 
@@ -313,12 +318,25 @@ int run_batch(hyobfs_salamander* c, const hyobfs_batch* b, void* stream, bool ob
     if (rc != HYOBFS_OK) return rc;
     std::unique_lock<std::mutex> ws_lk(c->ws_mu, std::defer_lock);
     uint64_t keys_off = 0;
+    const hyobfs::SideLane* side = nullptr;
     if (const uint64_t need = ctx_ws_bytes(c, b, keys_off)) {   // held through the launch (see StreamWs)
         ws_lk.lock();
-        auto* w = static_cast<uint8_t*>(stream_workspace(c, s, need));
+        hyobfs_salamander::StreamWs* e = nullptr;
+        auto* w = static_cast<uint8_t*>(stream_workspace(c, s, need, &e));
         if (!w) return HYOBFS_ERR_NOMEM;
         if (keys_off) bp.tile_sums = reinterpret_cast<uint64_t*>(w);
         if (need > keys_off) bp.keys = reinterpret_cast<uint64_t*>(w + keys_off);
+        if (bp.keys && hyobfs::resolve_kernel(c->kernel) == HYOBFS_KERNEL_PIPE) {
+            if (!e->side.s) {   // the side lane of this caller stream, kept until the context is freed
+                if (hipStreamCreateWithFlags(&e->side.s, hipStreamNonBlocking) != hipSuccess) {
+                    e->side.s = nullptr;
+                    return HYOBFS_ERR_HIP;
+                }
+                for (auto& ev : e->side.ev)
+                    if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return HYOBFS_ERR_HIP;
+            }
+            side = &e->side;
+        }
     }
 #ifdef HY_BOUNDS_CHECK
     // debug variant: HYOBFS_DEBUG_IN_BYTES bounds the input; report the first bad access
@@ -329,7 +347,7 @@ int run_batch(hyobfs_salamander* c, const hyobfs_batch* b, void* stream, bool ob
     bp.dbg = dbg;
     const char* ib = std::getenv("HYOBFS_DEBUG_IN_BYTES");
     bp.dbg_in_bytes = ib ? std::strtoull(ib, nullptr, 10) : ~0ull;
-    const int r2 = hyobfs::launch_salamander(obf, bp, c->kp, s) == hipSuccess ? HYOBFS_OK : HYOBFS_ERR_HIP;
+    const int r2 = hyobfs::launch_salamander(obf, bp, c->kp, s, side) == hipSuccess ? HYOBFS_OK : HYOBFS_ERR_HIP;
     unsigned long long h[16];
     (void)hipStreamSynchronize(s);
     (void)hipMemcpy(h, dbg, sizeof h, hipMemcpyDeviceToHost);
@@ -338,7 +356,7 @@ int run_batch(hyobfs_salamander* c, const hyobfs_batch* b, void* stream, bool ob
                      h[2], h[3], h[4], h[5], h[6], (unsigned long long)bp.n);
     return r2;
 #else
-    return hyobfs::launch_salamander(obf, bp, c->kp, s) == hipSuccess ? HYOBFS_OK : HYOBFS_ERR_HIP;
+    return hyobfs::launch_salamander(obf, bp, c->kp, s, side) == hipSuccess ? HYOBFS_OK : HYOBFS_ERR_HIP;
 #endif
 }
 
@@ -518,7 +536,12 @@ void hyobfs_salamander_free(hyobfs_salamander* c) {
         }
         // the callers' streams may be gone by now: wait for the whole device
         if (!c->ws.empty()) (void)hipDeviceSynchronize();
-        for (auto& e : c->ws) (void)hipFree(e.p);
+        for (auto& e : c->ws) {
+            (void)hipFree(e.p);
+            for (auto& ev : e.side.ev)
+                if (ev) (void)hipEventDestroy(ev);
+            if (e.side.s) (void)hipStreamDestroy(e.side.s);
+        }
         if (c->stage) (void)hipHostFree(c->stage);
         for (auto& sl : c->slot) {
             if (sl.s) {
@@ -539,7 +562,7 @@ void hyobfs_salamander_free(hyobfs_salamander* c) {
 int hyobfs_salamander_device(const hyobfs_salamander* c) { return c ? c->device : -1; }
 
 int hyobfs_salamander_set_kernel(hyobfs_salamander* c, int kernel) {
-    if (!c || kernel < HYOBFS_KERNEL_AUTO || kernel > HYOBFS_KERNEL_STREAM) return HYOBFS_ERR_INVALID;
+    if (!c || kernel < HYOBFS_KERNEL_AUTO || kernel > HYOBFS_KERNEL_PIPE) return HYOBFS_ERR_INVALID;
     c->kernel = kernel;
     return HYOBFS_OK;
 }

@@ -77,8 +77,16 @@ struct BatchParams {
 // HYOBFS_KERNEL_* that a context's setting resolves to (AUTO: the
 // HYOBFS_KERNEL environment variable, else 0)
 int resolve_kernel(int ctx_kernel);
+// Side lane of the pipelined two-pass path (HYOBFS_KERNEL_PIPE): a second
+// stream on the caller's device for the key pass, and the events that order
+// each sweep chunk after its keys.  Owned by the context, one per caller stream.
+constexpr int kSideEvents = 64;
+struct SideLane {
+    hipStream_t s = nullptr;
+    hipEvent_t ev[kSideEvents] = {};
+};
 hipError_t launch_salamander(bool obfuscate, const BatchParams& b, const KeyParams& k,
-                             hipStream_t s);
+                             hipStream_t s, const SideLane* side = nullptr);
 hipError_t launch_keys(const KeyParams& k, const uint64_t* salts, uint8_t* keys, uint64_t n,
                        hipStream_t s);
 hipError_t launch_gecko_encode(const KeyParams& k, const hyobfs_gecko_batch& b, hipStream_t s);

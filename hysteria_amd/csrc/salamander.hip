@@ -37,9 +37,9 @@ namespace hyobfs {
     extern template void launch_uniform_sw<false, n>(const BatchParams&, const KeyParams&, const UniformParams&,   \
                                                      hipStream_t);                                                  \
     extern template void launch_stream_sw<true, n>(const BatchParams&, const KeyParams&, const StreamParams&,      \
-                                                   uint64_t, uint64_t, hipStream_t);                                \
+                                                   uint64_t, uint64_t, hipStream_t, const SideLane*);               \
     extern template void launch_stream_sw<false, n>(const BatchParams&, const KeyParams&, const StreamParams&,     \
-                                                    uint64_t, uint64_t, hipStream_t);
+                                                    uint64_t, uint64_t, hipStream_t, const SideLane*);
 HY_EXTERN_SW(0) HY_EXTERN_SW(1) HY_EXTERN_SW(2) HY_EXTERN_SW(3) HY_EXTERN_SW(4) HY_EXTERN_SW(5)
 HY_EXTERN_SW(6) HY_EXTERN_SW(7) HY_EXTERN_SW(8) HY_EXTERN_SW(9) HY_EXTERN_SW(10) HY_EXTERN_SW(11)
 HY_EXTERN_SW(12) HY_EXTERN_SW(13) HY_EXTERN_SW(14) HY_EXTERN_SW(15)
@@ -171,6 +171,7 @@ static int kernel_override() {   // HYOBFS_KERNEL, as HYOBFS_KERNEL_* (0 = auto)
                : std::strcmp(e, "persistent") == 0   ? 2
                : std::strcmp(e, "uniform") == 0      ? 3
                : std::strcmp(e, "stream") == 0       ? 4
+               : std::strcmp(e, "pipe") == 0         ? 5
                                                       : 0;
     }
     return v;
@@ -204,19 +205,21 @@ static void launch_main(const BatchParams& bp, const KeyParams& k, hipStream_t s
 // uniform kernel; an odd last datagram through the wave kernel (its metadata
 // is reported by the uniform launch).
 template <bool OBF>
-static bool try_uniform(const BatchParams& b, const KeyParams& k, hipStream_t s) {
+static bool try_uniform(const BatchParams& b, const KeyParams& k, hipStream_t s, const SideLane* side) {
     // only when asked for: on 1M x 1200 B both measure slower than the wave
     // kernel (uniform 0.56 vs 0.50 ms, two-pass 0.47-0.62 vs 0.46)
     const int kc = kernel_choice(b);
-    if (kc != 3 && kc != 4) return false;
+    if (kc < 3 || kc > 5) return false;
     UniformParams P;
     StreamParams SP;
     uint32_t W = 0;
-    if (kc == 4 && stream_params<OBF>(b, SP)) {   // two passes: keys, then one-shot sweep
+    // two passes: keys, then one-shot sweep (pipe: keys on the side lane)
+    if (kc >= 4 && stream_params<OBF>(b, SP)) {
+        const SideLane* sl = kc == 5 ? side : nullptr;
         W = SP.W;
         switch (k.salt_pos >> 3) {
 #define HY_CASE(sw) \
-    case sw: launch_stream_sw<OBF, sw>(b, k, SP, b.n / 2, b.n, s); break;
+    case sw: launch_stream_sw<OBF, sw>(b, k, SP, b.n / 2, b.n, s, sl); break;
             HY_CASE(0) HY_CASE(1) HY_CASE(2) HY_CASE(3) HY_CASE(4) HY_CASE(5) HY_CASE(6) HY_CASE(7)
             HY_CASE(8) HY_CASE(9) HY_CASE(10) HY_CASE(11) HY_CASE(12) HY_CASE(13) HY_CASE(14)
             HY_CASE(15)
@@ -254,12 +257,13 @@ static bool try_uniform(const BatchParams& b, const KeyParams& k, hipStream_t s)
     return true;
 }
 
-hipError_t launch_salamander(bool obf, const BatchParams& b, const KeyParams& k, hipStream_t s) {
+hipError_t launch_salamander(bool obf, const BatchParams& b, const KeyParams& k, hipStream_t s,
+                             const SideLane* side) {
     if (b.n == 0) return hipSuccess;
     const uint64_t ntiles = div_up(b.n, kTile);
     if (ntiles > 0x7fffffffull) return hipErrorInvalidValue;
     if (k.nblk == 2 && (k.salt_pos >> 3) != 15) return hipErrorInvalidValue;   // by construction
-    if (obf ? try_uniform<true>(b, k, s) : try_uniform<false>(b, k, s)) return hipGetLastError();
+    if (obf ? try_uniform<true>(b, k, s, side) : try_uniform<false>(b, k, s, side)) return hipGetLastError();
     BatchParams bp = b;
     if (b.out_stride == 0) {
         const dim3 grid((uint32_t)ntiles), block(kTile);

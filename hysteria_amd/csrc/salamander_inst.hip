@@ -18,7 +18,7 @@ template void launch_wave_sw<false, false, HY_SW>(const BatchParams&, const KeyP
 template void launch_uniform_sw<true, HY_SW>(const BatchParams&, const KeyParams&, const UniformParams&, hipStream_t);
 template void launch_uniform_sw<false, HY_SW>(const BatchParams&, const KeyParams&, const UniformParams&, hipStream_t);
 template void launch_stream_sw<true, HY_SW>(const BatchParams&, const KeyParams&, const StreamParams&, uint64_t,
-                                            uint64_t, hipStream_t);
+                                            uint64_t, hipStream_t, const SideLane*);
 template void launch_stream_sw<false, HY_SW>(const BatchParams&, const KeyParams&, const StreamParams&, uint64_t,
-                                             uint64_t, hipStream_t);
+                                             uint64_t, hipStream_t, const SideLane*);
 }  // namespace hyobfs

@@ -205,6 +205,16 @@ __global__ __launch_bounds__(256) void salamander_stream_kernel(BatchParams B, K
         stream_sweep<OBF>(B, P, b - min(P.nkb, kb + 1));
 }
 
+// Key pass alone (HYOBFS_KERNEL_PIPE): a small grid, grid-stride over the
+// launch's key blocks, on the side lane's stream.  Its few waves hash beside
+// the memory-bound sweep of the previous chunk instead of sharing that grid:
+// in one grid the late key blocks held the launch open after its sweep waves
+// had drained.
+template <bool OBF, int SW>
+__global__ __launch_bounds__(256) void salamander_stream_keys_kernel(BatchParams B, KeyParams K, StreamParams P) {
+    for (uint64_t kb = blockIdx.x; kb < P.nkb; kb += gridDim.x) stream_keys<OBF, SW>(B, K, P, kb);
+}
+
 template <bool OBF>
 inline bool stream_params(const BatchParams& b, StreamParams& P) {
     UniformParams U;
@@ -237,11 +247,28 @@ inline uint64_t stream_env(const char* name, uint64_t dflt) {   // A/B knobs, re
     return v > 0 ? (uint64_t)v : dflt;
 }
 
+// Side-lane schedule (HYOBFS_KERNEL_PIPE) defaults: chunk 0 of 2048 runs
+// (4K datagrams) keyed by a full grid, then chunks up to 4x the previous one,
+// each keyed by at most 256 workgroups (one wave per SIMD) while the caller's
+// stream sweeps the chunk before it.
+#ifndef HY_PIPE_FIRST_RUNS
+#define HY_PIPE_FIRST_RUNS 2048
+#endif
+#ifndef HY_PIPE_GROW
+#define HY_PIPE_GROW 4
+#endif
+#ifndef HY_PIPE_KEY_BLOCKS
+#define HY_PIPE_KEY_BLOCKS 256
+#endif
+
 template <bool OBF, int SW>
 void launch_stream_sw(const BatchParams& bp, const KeyParams& k, const StreamParams& base, uint64_t nruns,
-                      uint64_t nkeys, hipStream_t s) {
-    static const uint64_t first = stream_env("HYOBFS_STREAM_FIRST_RUNS", HY_STREAM_FIRST_RUNS);
-    static const uint64_t grow = std::max<uint64_t>(2, stream_env("HYOBFS_STREAM_GROW", HY_STREAM_GROW));
+                      uint64_t nkeys, hipStream_t s, const SideLane* side) {
+    static const uint64_t s_first = stream_env("HYOBFS_STREAM_FIRST_RUNS", HY_STREAM_FIRST_RUNS);
+    static const uint64_t s_grow = std::max<uint64_t>(2, stream_env("HYOBFS_STREAM_GROW", HY_STREAM_GROW));
+    // the side-lane knobs are read per call (in-process A/B of schedules)
+    const uint64_t first = side ? stream_env("HYOBFS_PIPE_FIRST_RUNS", HY_PIPE_FIRST_RUNS) : s_first;
+    const uint64_t grow = side ? std::max<uint64_t>(2, stream_env("HYOBFS_PIPE_GROW", HY_PIPE_GROW)) : s_grow;
     // chunk i = runs [r[i], r[i+1])
     uint64_t r[64];
     int m = 0;
@@ -258,6 +285,35 @@ void launch_stream_sw(const BatchParams& bp, const KeyParams& k, const StreamPar
         P.kp1 = (i + 1 == m) ? nkeys : 2 * r[i + 1];
         P.nkb = (uint32_t)div_up(P.kp1 - P.kp0, 256);
     };
+    if (side) {
+        // side stream: after the caller's earlier work (the inputs), the keys of
+        // chunk 0, 1, ... back to back, event i+1 after chunk i's; caller's
+        // stream: sweep chunk i once event i+1 has fired.  Keys run ahead of the
+        // sweeps (a throttled grid still hashes ~8x faster than the sweep moves
+        // bytes), so only chunk 0's keys are exposed.
+        const uint64_t kblocks = stream_env("HYOBFS_PIPE_KEY_BLOCKS", HY_PIPE_KEY_BLOCKS);
+        if (hipEventRecord(side->ev[0], s) != hipSuccess) return;
+        if (hipStreamWaitEvent(side->s, side->ev[0], 0) != hipSuccess) return;
+        for (int i = 0; i < m; ++i) {
+            StreamParams P = base;
+            key_range(i, P);
+            const uint64_t grid = i == 0 ? P.nkb : std::min<uint64_t>(P.nkb, kblocks);
+            hipLaunchKernelGGL((salamander_stream_keys_kernel<OBF, SW>), dim3((uint32_t)grid),
+                               dim3(kGroup * kWavesPerBlock), 0, side->s, bp, k, P);
+            if (hipEventRecord(side->ev[i + 1], side->s) != hipSuccess) return;
+        }
+        for (int i = 0; i < m; ++i) {
+            StreamParams P = base;   // nkb = 0: every block sweeps
+            P.kstride = 1;
+            P.run0 = r[i];
+            P.nch = (r[i + 1] - r[i]) * P.CC;
+            const uint64_t blocks = div_up(div_up(P.nch, (uint64_t)kGroup * kSU), kWavesPerBlock);
+            if (hipStreamWaitEvent(s, side->ev[i + 1], 0) != hipSuccess) return;
+            hipLaunchKernelGGL((salamander_stream_kernel<OBF, SW>), dim3((uint32_t)blocks),
+                               dim3(kGroup * kWavesPerBlock), 0, s, bp, k, P);
+        }
+        return;
+    }
     for (int i = 0; i <= m; ++i) {   // launch i: keys of chunk i, sweep of chunk i - 1
         StreamParams P = base;
         if (i < m) key_range(i, P);

@@ -96,9 +96,12 @@ int hyobfs_salamander_device(const hyobfs_salamander* ctx);
    output, nothing dropped) two more kernels can be asked for:
    HYOBFS_KERNEL_UNIFORM (aligned-load sweep over runs of two datagrams) and
    HYOBFS_KERNEL_STREAM (keys pass into context scratch pipelined with one-shot
-   4 KiB sweeps); both measure slower than AUTO on 1M x 1200 B.  The
-   HYOBFS_KERNEL environment variable (wave|persistent|uniform|stream)
-   overrides AUTO.  UNIFORM or STREAM on a batch that is not uniform falls back
+   4 KiB sweeps); both measure slower than AUTO on 1M x 1200 B.
+   HYOBFS_KERNEL_PIPE is STREAM with the keys pass on a second stream the
+   context owns (one per caller stream), each sweep chunk ordered after its keys
+   by an event, so the key grid never holds a sweep launch open.  The
+   HYOBFS_KERNEL environment variable (wave|persistent|uniform|stream|pipe)
+   overrides AUTO.  UNIFORM, STREAM or PIPE on a batch that is not uniform falls back
    to the AUTO choice.  Returns HYOBFS_ERR_INVALID for an unknown value.
    Outputs are identical. */
 enum {
@@ -106,7 +109,8 @@ enum {
     HYOBFS_KERNEL_WAVE = 1,
     HYOBFS_KERNEL_PERSISTENT = 2,
     HYOBFS_KERNEL_UNIFORM = 3,
-    HYOBFS_KERNEL_STREAM = 4
+    HYOBFS_KERNEL_STREAM = 4,
+    HYOBFS_KERNEL_PIPE = 5
 };
 int hyobfs_salamander_set_kernel(hyobfs_salamander* ctx, int kernel);
 

@@ -39,6 +39,9 @@ SPECS = {
     "test_emulated_stream_kernel_pipelined": lambda p: (
         "uniform", p["args"], {"HYOBFS_KERNEL": "stream", "HYEMU_CUS": "2", "HYOBFS_STREAM_FIRST_RUNS": "12",
                                "HYOBFS_STREAM_GROW": "2"}),
+    "test_emulated_pipe_kernel": lambda p: (
+        "uniform", p["args"], {"HYOBFS_KERNEL": "pipe", "HYEMU_CUS": "2", "HYOBFS_PIPE_FIRST_RUNS": "12",
+                               "HYOBFS_PIPE_GROW": "2", "HYOBFS_PIPE_KEY_BLOCKS": "1"}),
     "test_emulated_wave_kernel_run_lengths": lambda p: (
         p["which"], p["args"], {"HYOBFS_RUN_LOG2": p["run_log2"], "HYOBFS_KERNEL": "wave"}),
     "test_emulated_wave_kernel_packed_run_lengths": lambda p: (
@@ -167,6 +170,14 @@ def test_emulated_stream_kernel_pipelined(emu_lib, args):
                                     "HYOBFS_STREAM_FIRST_RUNS": "12", "HYOBFS_STREAM_GROW": "2"})
 
 
+
+
+@pytest.mark.parametrize("args", ["1001 1200 0", "1000 1200 1", "999 1192 1", "64 16 1"])
+def test_emulated_pipe_kernel(emu_lib, args):
+    """HYOBFS_KERNEL_PIPE: keys of every chunk on the side lane (chunk 0 by a full
+    grid, later chunks grid-striding over one workgroup), sweeps on the caller's stream."""
+    _run(emu_lib, "uniform", args, {"HYOBFS_KERNEL": "pipe", "HYEMU_CUS": "2", "HYOBFS_PIPE_FIRST_RUNS": "12",
+                                    "HYOBFS_PIPE_GROW": "2", "HYOBFS_PIPE_KEY_BLOCKS": "1"})
 
 
 @pytest.mark.parametrize("which,args,run_log2", RUN_CASES)
