@@ -67,6 +67,8 @@ struct BatchParams {
     uint64_t part_len;            // main kernel: n / grid datagrams per workgroup ...
     uint64_t part_rem;            // ... plus one for the first n % grid workgroups
     uint32_t run_log2;            // wave kernel: datagrams per run = 2^run_log2
+    uint32_t tile_stride;         // persistent kernel: 0 = one contiguous part per workgroup;
+                                  // G = workgroup g takes the 256-datagram tiles g, g+G, g+2G, ...
     int kernel;                   // HYOBFS_KERNEL_* of the context (0 = auto)
     // HY_BOUNDS_CHECK builds only (build_variants/, never the shipped library):
     // first out-of-range access recorded here instead of performed

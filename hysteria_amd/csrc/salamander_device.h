@@ -473,12 +473,32 @@ __global__ HY_MAIN_BOUNDS void salamander_kernel(BatchParams B, KeyParams K) {
     __shared__ uint32_t s_max[kTile / 64];
 
     const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
-    // balanced static partition: the first part_rem workgroups take one extra datagram
     const uint64_t g = blockIdx.x;
-    const uint64_t P0 = g * B.part_len + min<uint64_t>(g, B.part_rem);
-    const uint64_t P1 = P0 + B.part_len + (g < B.part_rem ? 1 : 0);
-    if (P0 >= P1) return;
-    const uint32_t nsub = (uint32_t)((P1 - P0 + kTile - 1) / kTile);
+    // Work order.  Contiguous: a balanced static partition (the first part_rem
+    // workgroups take one extra datagram), sub-tiles of 256 from P0.  Strided
+    // (tile_stride = G): sub-tile s is the batch's tile g + s G, so the resident
+    // workgroups sweep neighbouring tiles at any moment (an address window of
+    // G tiles instead of the whole batch) and a packed tile's output offset is
+    // its tile prefix.
+    const uint64_t G = B.tile_stride;
+    const bool strided = G != 0;
+    uint64_t P0 = 0, P1 = B.n;
+    uint32_t nsub;
+    if (strided) {
+        const uint64_t ntiles = (B.n + kTile - 1) / kTile;
+        if (g >= ntiles) return;
+        nsub = (uint32_t)((ntiles - 1 - g) / G + 1);
+    } else {
+        P0 = g * B.part_len + min<uint64_t>(g, B.part_rem);
+        P1 = P0 + B.part_len + (g < B.part_rem ? 1 : 0);
+        if (P0 >= P1) return;
+        nsub = (uint32_t)((P1 - P0 + kTile - 1) / kTile);
+    }
+    // first datagram of sub-tile s, and one past its last
+    auto sub_first = [&](uint32_t s) -> uint64_t {
+        return strided ? (g + (uint64_t)s * G) * kTile : P0 + (uint64_t)s * kTile;
+    };
+    auto sub_end = [&](uint64_t ps) -> uint64_t { return min<uint64_t>(ps + kTile, P1); };
     const uint8_t* __restrict__ in = B.in;
     const uint32_t nsteps = 12 * K.nblk;
 
@@ -501,7 +521,7 @@ __global__ HY_MAIN_BOUNDS void salamander_kernel(BatchParams B, KeyParams K) {
 
     // output offset of datagram P0 (packed layout)
     uint64_t carry = 0;
-    if (PACKED) {
+    if (PACKED && !strided) {
         const uint64_t tb = P0 / kTile * kTile;
         uint32_t Wt = 0;
         if (tb + t < P0) Wt = out_width<OBF>(pkt_len(B, tb + t), B.pkt_cap);
@@ -517,11 +537,11 @@ __global__ HY_MAIN_BOUNDS void salamander_kernel(BatchParams B, KeyParams K) {
     HashState<SW> hs;
 
     auto prep_load = [&](uint32_t s) {   // issue the global loads of sub-tile s
-        pp = P0 + (uint64_t)s * kTile + t;
+        pp = sub_first(s) + t;
         pL = 0;
         pioff = 0;
         psalt = 0;
-        if (pp < P1) {
+        if (pp < sub_end(sub_first(s))) {
             pL = pkt_len(B, pp);
             pioff = pkt_in_off(B, pp);
             if (OBF) psalt = B.salts[pp];
@@ -529,13 +549,14 @@ __global__ HY_MAIN_BOUNDS void salamander_kernel(BatchParams B, KeyParams K) {
     };
     // widths, offsets, drop rules, LDS metadata of sub-tile s (has __syncthreads)
     auto prep_finish = [&](uint32_t s, TileBuf& T) {
-        const uint64_t ps = P0 + (uint64_t)s * kTile;
-        const uint32_t cnt = (uint32_t)min<uint64_t>(kTile, P1 - ps);
+        const uint64_t ps = sub_first(s);
+        const uint32_t cnt = (uint32_t)(sub_end(ps) - ps);
         const bool live = (uint32_t)t < cnt;
         uint32_t W = live ? out_width<OBF>(pL, B.pkt_cap) : 0u;
         uint64_t ooff, first;
         if (PACKED) {
             uint64_t tot;
+            if (strided) carry = B.tile_prefix[ps / kTile];   // ps is a tile start
             ooff = carry + block_scan(W, tot);
             first = carry;
             carry += tot;
@@ -698,6 +719,10 @@ __global__ HY_MAIN_BOUNDS void salamander_kernel(BatchParams B, KeyParams K) {
     }
 }
 
+#ifndef HY_PERSIST_STRIDED
+#define HY_PERSIST_STRIDED 0
+#endif
+
 // Resident workgroups per CU of one main-kernel instantiation (persistent grid).
 template <bool OBF, bool PACKED, int SW>
 int resident_per_cu() {
@@ -725,10 +750,14 @@ template <bool OBF, bool PACKED, int SW>
 void launch_main_sw(const BatchParams& bp, const KeyParams& k, hipStream_t s) {
     // every workgroup resident (static partition), at least a wave of datagrams each
     const uint64_t full = (uint64_t)device_cus() * resident_per_cu<OBF, PACKED, SW>();
-    const uint64_t grid = std::min<uint64_t>(full, div_up(bp.n, 64));
+    // HYOBFS_PERSIST_ORDER=strided|contiguous (read per launch: in-process A/B)
+    const char* e = std::getenv("HYOBFS_PERSIST_ORDER");
+    const bool strided = e ? std::strcmp(e, "strided") == 0 : HY_PERSIST_STRIDED;
+    const uint64_t grid = std::min<uint64_t>(full, strided ? div_up(bp.n, kTile) : div_up(bp.n, 64));
     BatchParams b = bp;
     b.part_len = bp.n / grid;
     b.part_rem = bp.n % grid;
+    b.tile_stride = strided ? (uint32_t)grid : 0u;
     hipLaunchKernelGGL((salamander_kernel<OBF, PACKED, SW>), dim3((uint32_t)grid), dim3(kTile), 0, s, b, k);
 }
 

@@ -12,8 +12,9 @@ import torch  # noqa: E402
 
 from hysteria_amd import _lib  # noqa: E402
 
-# each argument: path/to/lib.so[:kernel]  (kernel = auto|wave|persistent|uniform)
-KERNELS = {"auto": 0, "wave": 1, "persistent": 2, "uniform": 3, "stream": 4}
+# each argument: path/to/lib.so[:kernel[:VAR=value,...]]  (kernel = auto|wave|persistent|uniform|stream|pipe;
+# the variables are set for that variant's launches only: per-launch knobs such as HYOBFS_PERSIST_ORDER)
+KERNELS = {"auto": 0, "wave": 1, "persistent": 2, "uniform": 3, "stream": 4, "pipe": 5}
 specs = [a.split(":") for a in (sys.argv[1:] or ["hysteria_amd/libhyobfs.so"])]
 libs = [x[0] for x in specs]
 P, L = 1 << 20, int(os.environ.get("AB_LEN", "1200"))
@@ -33,7 +34,17 @@ for spec in specs:
     assert lib.hyobfs_salamander_new(psk, len(psk), 0, ctypes.byref(h)) == 0
     kern = spec[1] if len(spec) > 1 else "auto"
     assert lib.hyobfs_salamander_set_kernel(h, KERNELS[kern]) == 0
-    handles.append((os.path.basename(path).replace("libhyobfs_", "").replace(".so", "") + ":" + kern, lib, h))
+    env = dict(kv.split("=", 1) for kv in spec[2].split(",")) if len(spec) > 2 else {}
+    name = os.path.basename(path).replace("libhyobfs_", "").replace(".so", "") + ":" + kern
+    name += (":" + ",".join(f"{k}={v}" for k, v in env.items())) if env else ""
+    handles.append((name, lib, h, env))
+ENV_KEYS = {k for x in handles for k in x[3]}
+
+
+def use_env(env):
+    for k in ENV_KEYS:
+        os.environ.pop(k, None)
+    os.environ.update(env)
 
 if workload == "uniform":
     inp = torch.empty(P * L, dtype=torch.uint8, device=dev)
@@ -73,9 +84,22 @@ else:
 
 K = int(os.environ.get("AB_STEPS", "10"))
 R = int(os.environ.get("AB_ROUNDS", "6"))
-res = {name: {"obf": [], "deobf": []} for name, _, _ in handles}
+res = {name: {"obf": [], "deobf": []} for name, _, _, _ in handles}
+# every variant's wire must equal the first one's before timing
+ref = None
+for name, lib, h, env in handles:
+    use_env(env)
+    wire.zero_()
+    lib.hyobfs_salamander_obfuscate_batch(h, ctypes.byref(bo), None)
+    torch.cuda.synchronize()
+    if ref is None:
+        ref = wire.clone()
+    assert torch.equal(wire, ref), f"{name}: wire differs from {handles[0][0]}"
+del ref
+print("wire identical across variants")
 for r in range(R + 1):
-    for name, lib, h in handles:
+    for name, lib, h, env in handles:
+        use_env(env)
         for kind, fn, b in (("obf", lib.hyobfs_salamander_obfuscate_batch, bo),
                             ("deobf", lib.hyobfs_salamander_deobfuscate_batch, bd)):
             fn(h, ctypes.byref(b), None)

@@ -49,6 +49,9 @@ SPECS = {
                                 "HYOBFS_KERNEL": "wave"}),
     "test_emulated_persistent_kernel": lambda p: None if p["which"] in ("conn", "host", "coalesce", "quic") else (
         p["which"], p["args"], {"HYEMU_CUS": p["cus"], "HYOBFS_KERNEL": "persistent"}),
+    "test_emulated_persistent_kernel_strided": lambda p: (
+        p["which"], p["args"], {"HYEMU_CUS": p["cus"], "HYOBFS_KERNEL": "persistent",
+                                "HYOBFS_PERSIST_ORDER": "strided"}),
     "test_emulated_kernel_vs_oracle": lambda p: (p["which"], p["args"], {"HYEMU_CUS": p["cus"]}),
 }
 
@@ -191,6 +194,17 @@ def test_emulated_wave_kernel_packed_run_lengths(emu_lib, which, args, run_log2)
     base is the tile prefix plus the widths of the tile's earlier datagrams."""
     _run(emu_lib, which, args, {"HYOBFS_PACKED_RUN_LOG2": run_log2, "HYOBFS_RUN_LOG2": run_log2,
                                 "HYOBFS_KERNEL": "wave"})
+
+
+# the persistent kernel with interleaved tiles (workgroup g: tiles g, g+G, ...)
+STRIDED_CASES = [c for c in CASES if c[0] in ("uniform", "bimodal", "ragged", "far")]
+
+
+@pytest.mark.parametrize("which,args,cus", STRIDED_CASES)
+def test_emulated_persistent_kernel_strided(emu_lib, which, args, cus):
+    """HYOBFS_PERSIST_ORDER=strided: each packed tile's offset from the tile prefix,
+    tiles of one workgroup G apart (edge chunks shared between workgroups)."""
+    _run(emu_lib, which, args, {"HYEMU_CUS": cus, "HYOBFS_KERNEL": "persistent", "HYOBFS_PERSIST_ORDER": "strided"})
 
 
 @pytest.mark.parametrize("which,args,cus", CASES)
