@@ -299,6 +299,10 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t x) {
 // --------------------------------------------------------------- main kernel
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
+#ifndef HY_PERSIST_PARK
+#define HY_PERSIST_PARK 1   // A/B: 0 = boundary chunks stored by their owner with byte masks
+#endif
+
 struct TileBuf {                 // one sub-tile of <= kTile datagrams, in LDS
     uint32_t o[kTile];           // output region start, relative to base
     uint32_t w[kTile];           // output region width, 0 = dropped
@@ -469,6 +473,13 @@ __global__ HY_MAIN_BOUNDS void salamander_kernel(BatchParams B, KeyParams K) {
     constexpr int U = kU;
 
     __shared__ TileBuf buf[2];
+#if HY_PERSIST_PARK
+    // packed layout: complete boundary chunks parked here by their owner (up to 3
+    // per datagram: first, second, last chunk), stored by the sweep lane that
+    // covers them, so their lines leave in the sweep's own store instructions
+    __shared__ uint4 s_park[3 * kTile];
+    __shared__ uint32_t s_parkm[kTile];   // bit i: candidate i of datagram t is parked
+#endif
     __shared__ uint64_t s_sum[kTile / 64];
     __shared__ uint32_t s_max[kTile / 64];
 
@@ -658,6 +669,22 @@ __global__ HY_MAIN_BOUNDS void salamander_kernel(BatchParams B, KeyParams K) {
         auto retire = [&](uint32_t it, const SweepRegs& R) {
 #pragma unroll
             for (int u = 0; u < U; ++u) {
+#if HY_PERSIST_PARK
+                if (PACKED && !R.fast[u]) {   // a parked boundary chunk of datagram q?
+                    const uint32_t c = it * (kTile * U) + u * kTile + t;
+                    const uint32_t q = R.q[u], m = c < nchunks ? s_parkm[q] : 0u;
+                    if (m) {
+                        const uint32_t cs = T.o[q] >> 4, ce = (T.o[q] + T.w[q] - 1) >> 4;
+                        const int i = c == cs ? 0 : c == cs + 1 ? 1 : c == ce ? 2 : 3;
+                        if (i < 3 && (m >> i & 1)) {
+                            const uint4 pv = s_park[3 * q + i];
+                            u128 v;
+                            __builtin_memcpy(&v, &pv, 16);
+                            store16_stream(outb + (c << 4), v);
+                        }
+                    }
+                }
+#endif
                 if (!R.fast[u]) continue;
                 const uint32_t a = (it * (kTile * U) + u * kTile + t) << 4;
                 const uint4 kk = T.key[2 * R.q[u] + ((a >> 4) & 1)];
@@ -672,6 +699,9 @@ __global__ HY_MAIN_BOUNDS void salamander_kernel(BatchParams B, KeyParams K) {
         const uint32_t steps = has_next ? nsteps : 0u;
         if (has_next) prep_load(s + 1);
         auto boundary = [&]() {   // chunks datagram t owns that are not inside one payload
+#if HY_PERSIST_PARK
+            uint32_t pm = 0;
+#endif
             if ((uint32_t)t < cnt && T.w[t]) {
                 const uint32_t st = T.o[t], en = st + T.w[t];
                 const uint32_t cs = st >> 4, ce = (en - 1) >> 4;
@@ -686,11 +716,22 @@ __global__ HY_MAIN_BOUNDS void salamander_kernel(BatchParams B, KeyParams K) {
                     u128 r = 0;
                     uint32_t cov = 0;
                     for (uint32_t k = t; k < cnt && T.o[k] < a + 16; ++k) chunk_contrib<OBF>(B, T, in, k, a, r, cov);
+#if HY_PERSIST_PARK
+                    if (PACKED && cov == 0xFFFFu) {   // complete: the sweep stores it
+                        s_park[3 * t + i] = make_uint4((uint32_t)r, (uint32_t)(r >> 32), (uint32_t)(r >> 64),
+                                                       (uint32_t)(r >> 96));
+                        pm |= 1u << i;
+                        continue;
+                    }
+#endif
                     if (cov && HY_OK(3, (uint64_t)(outb - B.out) + a + 16 <= B.out_cap + 15, (uint64_t)(outb - B.out),
                                      a, cov, s))
                         store_masked(outb + a, r, cov);
                 }
             }
+#if HY_PERSIST_PARK
+            s_parkm[t] = pm;
+#endif
         };
         // Sweep iteration it: issue its loads; while they fly, finish the
         // boundary chunks (iteration 0) and run one round of the next
@@ -700,7 +741,12 @@ __global__ HY_MAIN_BOUNDS void salamander_kernel(BatchParams B, KeyParams K) {
         for (uint32_t it = 0; it < n_loop; ++it) {
             SweepRegs R;
             if (it < n_iters) issue(it, R);
-            if (it == 0) boundary();
+            if (it == 0) {
+                boundary();
+#if HY_PERSIST_PARK
+                if (PACKED) __syncthreads();   // parked chunks visible to every sweep lane
+#endif
+            }
             if (it >= 1 && it <= steps) hash_step<SW>(hs, K, it - 1);
             if (it < n_iters) retire(it, R);
             if (it == 0 && has_next) {

@@ -150,7 +150,7 @@ def run_conn_scenarios(device: int = 0, batch: int = 64, n_batch: int = 200):
 
 
 def run_coalesce_scenarios(device: int = 0, writers: int = 8, per_writer: int = 300, readers: int = 4,
-                           max_batch: int = 64, max_wait_us: int = 200):
+                           max_batch: int = 64, max_wait_us: int = 200, idle_timeout: float = 3.0):
     """Coalescing mode (hyobfs_conn_set_coalescing): many threads calling the
     per-datagram WriteTo / ReadFrom of one connection share GPU batches.  Every
     datagram arrives exactly once with the reference's per-datagram semantics
@@ -193,7 +193,7 @@ def run_coalesce_scenarios(device: int = 0, writers: int = 8, per_writer: int = 
                 expect[key] = expect.get(key, 0) + 1
         total = sum(expect.values())
         got, lock = {}, threading.Lock()
-        cb.settimeout(3.0)   # readers left over once every datagram arrived end on this
+        cb.settimeout(idle_timeout)   # readers left over once every datagram arrived end on this
 
         def reader():
             while True:

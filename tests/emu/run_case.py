@@ -278,7 +278,8 @@ if __name__ == "__main__":
     elif which == "coalesce":
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         from conn_cases import run_coalesce_scenarios
-        run_coalesce_scenarios(writers=args[0], per_writer=args[1], readers=args[2], max_batch=args[3])
+        run_coalesce_scenarios(writers=args[0], per_writer=args[1], readers=args[2], max_batch=args[3],
+                               idle_timeout=30.0)   # emulated batches run slowly under a loaded CPU tier
     elif which == "far":
         case_slotted_far(args[0], args[1], args[2], bool(args[3]))
     elif which == "ragged":

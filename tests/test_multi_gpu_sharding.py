@@ -1,9 +1,16 @@
 """Multi-GPU path on CPU: the packet-index shards of hysteria_amd.shard cover the
 batch exactly once, and W = 2 ranks under torch.distributed (gloo), each running
 the oracle on its own shard, produce outputs whose concatenation is the
-single-process output.  The GPU path uses the same shard functions (bench.py)."""
+single-process output.  The same split through the PRODUCT: two rank processes
+each run their shard through the CPU-emulated build of the HIP library
+(tests/emu, the kernel sources compiled for the host), and on the GPU tier
+through the HIP library itself (test_gpu_two_rank_processes_product_shards).
+The GPU path uses the same shard functions (bench.py)."""
+import glob
 import os
 import socket
+import subprocess
+import sys
 
 import numpy as np
 import pytest
@@ -101,3 +108,63 @@ def test_c_abi_shard_bounds_match_host_mirror(world):
     for n in (0, 1, 7, 1 << 20):
         u = shard_bounds(None, n, world)
         assert u == [even_split(n, world, r)[0] for r in range(world)] + [n]
+
+
+def _run_ranks(mode, n, outdir, world=2, extra_env=None, timeout=300):
+    """Start `world` rank processes of tests/shard_rank.py; rank 0 leaves joined.bin."""
+    port = _free_port()
+    procs = []
+    for r in range(world):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port), **(extra_env or {}))
+        procs.append(subprocess.Popen([sys.executable, os.path.join(os.path.dirname(__file__), "shard_rank.py"),
+                                       mode, str(n), str(outdir)], env=env, stdout=subprocess.PIPE,
+                                      stderr=subprocess.STDOUT, text=True))
+    outs = []
+    for p in procs:
+        try:
+            outs.append(p.communicate(timeout=timeout)[0])
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            raise
+    assert all(p.returncode == 0 for p in procs), [o[-2000:] for o in outs]
+
+
+def _oracle_whole(n):
+    co = ref.COracle()
+    lens = ref.bimodal_lengths(3, 0, n)
+    in_off = np.zeros(n, np.uint64)
+    in_off[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+    inp = co.fill_stream(1, 0, int(lens.sum()) + 16)
+    whole, _, _, _ = co.batch(True, PSK, n, inp, in_off=in_off, in_len=lens, salts=co.salts(2, 0, n),
+                              out_cap=int(lens.sum()) + 8 * n)
+    return whole.tobytes()
+
+
+def test_gloo_two_ranks_emulated_product_shards(tmp_path):
+    """Two rank processes, each obfuscating its byte-balanced shard of a bimodal batch
+    with the product kernels (CPU-emulated build, ASan); joined = the oracle's whole batch."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    lib = os.path.join(root, "tests", "emu", "libhyobfs_emu.so")
+    asan = sorted(glob.glob("/opt/rocm/llvm/lib/clang/*/lib/linux/libclang_rt.asan-x86_64.so"))
+    if not asan or not os.path.exists("/opt/rocm/llvm/bin/clang++"):
+        pytest.skip("clang/ASan runtime not available")
+    srcs = glob.glob(os.path.join(root, "hysteria_amd", "csrc", "*")) + [os.path.join(root, "tests", "emu", "hip_emu.h")]
+    if not os.path.exists(lib) or os.path.getmtime(lib) < max(os.path.getmtime(x) for x in srcs):
+        subprocess.run([os.path.join(root, "tests", "emu", "build.sh")], check=True, capture_output=True)
+    n = 2000
+    _run_ranks("emu", n, tmp_path, extra_env={"HYOBFS_LIB": lib, "LD_PRELOAD": asan[-1],
+                                              "ASAN_OPTIONS": "detect_leaks=0", "HYEMU_CUS": "2"})
+    assert (tmp_path / "joined.bin").read_bytes() == _oracle_whole(n)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 3])
+def test_gpu_rank_processes_product_shards(tmp_path, world):
+    """bench.py's N-process layout on the GPU box: `world` rank processes (ranks map to
+    GPUs modulo the visible devices), each runs its shard of a 200k-datagram bimodal
+    batch through the HIP library; the gathered wire equals the oracle's whole batch."""
+    n = 200_000
+    _run_ranks("gpu", n, tmp_path, world=world, timeout=110)
+    assert (tmp_path / "joined.bin").read_bytes() == _oracle_whole(n)
