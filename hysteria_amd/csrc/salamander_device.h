@@ -300,7 +300,7 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t x) {
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 #ifndef HY_PERSIST_PARK
-#define HY_PERSIST_PARK 1   // A/B: 0 = boundary chunks stored by their owner with byte masks
+#define HY_PERSIST_PARK 0   // A/B: 1 = complete boundary chunks parked in LDS, stored by the sweep
 #endif
 
 struct TileBuf {                 // one sub-tile of <= kTile datagrams, in LDS
@@ -669,30 +669,33 @@ __global__ HY_MAIN_BOUNDS void salamander_kernel(BatchParams B, KeyParams K) {
         auto retire = [&](uint32_t it, const SweepRegs& R) {
 #pragma unroll
             for (int u = 0; u < U; ++u) {
+                u128 v = R.v[u];
 #if HY_PERSIST_PARK
+                bool parked = false;
                 if (PACKED && !R.fast[u]) {   // a parked boundary chunk of datagram q?
                     const uint32_t c = it * (kTile * U) + u * kTile + t;
                     const uint32_t q = R.q[u], m = c < nchunks ? s_parkm[q] : 0u;
                     if (m) {
                         const uint32_t cs = T.o[q] >> 4, ce = (T.o[q] + T.w[q] - 1) >> 4;
                         const int i = c == cs ? 0 : c == cs + 1 ? 1 : c == ce ? 2 : 3;
-                        if (i < 3 && (m >> i & 1)) {
+                        if (i < 3 && (m >> i & 1)) {   // stored pre-XORed with the key half below
                             const uint4 pv = s_park[3 * q + i];
-                            u128 v;
                             __builtin_memcpy(&v, &pv, 16);
-                            store16_stream(outb + (c << 4), v);
+                            parked = true;
                         }
                     }
                 }
-#endif
+                if (!R.fast[u] && !parked) continue;   // one store instruction for both
+#else
                 if (!R.fast[u]) continue;
+#endif
                 const uint32_t a = (it * (kTile * U) + u * kTile + t) << 4;
                 const uint4 kk = T.key[2 * R.q[u] + ((a >> 4) & 1)];
                 u128 k128;
                 __builtin_memcpy(&k128, &kk, 16);
                 if (HY_OK(2, (uint64_t)(outb - B.out) + a + 16 <= B.out_cap, (uint64_t)(outb - B.out), a,
                           nchunks, ((uint64_t)R.q[u] << 32) | (uint32_t)s))
-                    store16_stream(outb + a, R.v[u] ^ k128);
+                    store16_stream(outb + a, v ^ k128);
             }
         };
 
@@ -717,9 +720,13 @@ __global__ HY_MAIN_BOUNDS void salamander_kernel(BatchParams B, KeyParams K) {
                     uint32_t cov = 0;
                     for (uint32_t k = t; k < cnt && T.o[k] < a + 16; ++k) chunk_contrib<OBF>(B, T, in, k, a, r, cov);
 #if HY_PERSIST_PARK
-                    if (PACKED && cov == 0xFFFFu) {   // complete: the sweep stores it
-                        s_park[3 * t + i] = make_uint4((uint32_t)r, (uint32_t)(r >> 32), (uint32_t)(r >> 64),
-                                                       (uint32_t)(r >> 96));
+                    if (PACKED && cov == 0xFFFFu) {   // complete: the sweep stores it (XORing the key half again)
+                        const uint4 kk = T.key[2 * t + ((a >> 4) & 1)];
+                        u128 k128;
+                        __builtin_memcpy(&k128, &kk, 16);
+                        const u128 x = r ^ k128;
+                        s_park[3 * t + i] = make_uint4((uint32_t)x, (uint32_t)(x >> 32), (uint32_t)(x >> 64),
+                                                       (uint32_t)(x >> 96));
                         pm |= 1u << i;
                         continue;
                     }
