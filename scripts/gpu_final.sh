@@ -11,5 +11,5 @@ step smoke 200 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.
 step pytest 900 python -u -m pytest tests -x -v -m gpu --timeout 120 --timeout-method thread > $O/pytest_gpu.log 2>&1
 step collect 900 bash scripts/collect_profiles.sh $TAG > $O/collect.log 2>&1
 cp $O/profiles/pmc_traffic.json profiles/pmc_traffic.json
-step bench 300 python bench.py > $O/bench.json 2> $O/bench.err
+step bench 300 python bench.py > $O/bench.out 2> $O/bench.err && grep "^{" $O/bench.out > $O/bench.json
 echo done
