@@ -562,7 +562,7 @@ void hyobfs_salamander_free(hyobfs_salamander* c) {
 int hyobfs_salamander_device(const hyobfs_salamander* c) { return c ? c->device : -1; }
 
 int hyobfs_salamander_set_kernel(hyobfs_salamander* c, int kernel) {
-    if (!c || kernel < HYOBFS_KERNEL_AUTO || kernel > HYOBFS_KERNEL_PIPE) return HYOBFS_ERR_INVALID;
+    if (!c || kernel < HYOBFS_KERNEL_AUTO || kernel > HYOBFS_KERNEL_FLAT) return HYOBFS_ERR_INVALID;
     c->kernel = kernel;
     return HYOBFS_OK;
 }

@@ -30,6 +30,7 @@ __device__ __forceinline__ void hy_wave_sync() {
 
 constexpr int kTile = 256;          // datagrams per workgroup tile (= threads)
 constexpr uint32_t kMaxDatagram = (1u << 24) - 64;  // longest datagram a batch accepts
+constexpr int HY_KERNEL_FLAT = 6;   // HYOBFS_KERNEL_FLAT: the wave kernel's boundary-free sweep
 constexpr uint64_t kMaxStride = 1ull << 24;         // longest slot of a slotted output
 
 // BLAKE2b state for the per-packet key, precomputed on the host from the PSK

@@ -172,6 +172,7 @@ static int kernel_override() {   // HYOBFS_KERNEL, as HYOBFS_KERNEL_* (0 = auto)
                : std::strcmp(e, "uniform") == 0      ? 3
                : std::strcmp(e, "stream") == 0       ? 4
                : std::strcmp(e, "pipe") == 0         ? 5
+               : std::strcmp(e, "flat") == 0         ? 6
                                                       : 0;
     }
     return v;
@@ -184,15 +185,17 @@ int resolve_kernel(int ctx_kernel) { return ctx_kernel ? ctx_kernel : kernel_ove
 template <bool OBF, bool PACKED>
 static void launch_main(const BatchParams& bp, const KeyParams& k, hipStream_t s) {
     const int kc = kernel_choice(bp);
-    const int ov = kc == 1 ? 1 : kc == 2 ? 0 : -1;   // uniform / auto: per layout
+    const int ov = (kc == 1 || kc == HY_KERNEL_FLAT) ? 1 : kc == 2 ? 0 : -1;   // uniform / auto: per layout
     const bool wave = ov >= 0 ? ov == 1 : !PACKED;
+    BatchParams b = bp;
+    b.kernel = kc;   // resolved (context or HYOBFS_KERNEL): the wave launcher picks its sweep from it
     switch (k.salt_pos >> 3) {
-#define HY_CASE(n)                                    \
-    case n:                                           \
-        if (wave)                                     \
-            launch_wave_sw<OBF, PACKED, n>(bp, k, s); \
-        else                                          \
-            launch_main_sw<OBF, PACKED, n>(bp, k, s); \
+#define HY_CASE(n)                                   \
+    case n:                                          \
+        if (wave)                                    \
+            launch_wave_sw<OBF, PACKED, n>(b, k, s); \
+        else                                         \
+            launch_main_sw<OBF, PACKED, n>(b, k, s); \
         break;
         HY_CASE(0) HY_CASE(1) HY_CASE(2) HY_CASE(3) HY_CASE(4) HY_CASE(5) HY_CASE(6) HY_CASE(7)
         HY_CASE(8) HY_CASE(9) HY_CASE(10) HY_CASE(11) HY_CASE(12) HY_CASE(13) HY_CASE(14)

@@ -35,6 +35,12 @@ constexpr int kWavesPerBlock = 4;    // independent waves per workgroup
 #define HY_WU 8
 #endif
 constexpr int kWU = HY_WU;           // chunks per lane per sweep iteration
+#ifndef HY_FLAT_U
+#define HY_FLAT_U 4                  // the boundary-free sweep: chunks per lane per iteration
+#endif
+#ifndef HY_FLAT_MIN_WAVES
+#define HY_FLAT_MIN_WAVES 6          // ... and its waves per SIMD (two windows per chunk need registers)
+#endif
 #ifndef HY_RUN_LOG2
 #define HY_RUN_LOG2 3
 #endif
@@ -235,9 +241,11 @@ __device__ __forceinline__ uint32_t park_index(uint2 ow, uint32_t c) {
     return c == cs ? 0u : (c == cs + 1 && cs + 1 <= ce) ? 1u : (c == ce && ce > cs + 1) ? 2u : 3u;
 }
 
-template <bool OBF, bool PACKED, int SW>
-__global__ __launch_bounds__(kGroup* kWavesPerBlock, HY_WAVE_MIN_WAVES) void salamander_wave_kernel(BatchParams B,
-                                                                                                    KeyParams K) {
+// FLAT = the boundary-free sweep (flat_sweep below) for slotted batches whose
+// datagrams all have regions of 16 bytes or more and none is dropped.
+template <bool OBF, bool PACKED, int SW, bool FLAT = false>
+__global__ __launch_bounds__(kGroup* kWavesPerBlock, FLAT ? HY_FLAT_MIN_WAVES : HY_WAVE_MIN_WAVES) void
+salamander_wave_kernel(BatchParams B, KeyParams K) {
     constexpr uint32_t SALT = OBF ? 8u : 0u;   // salt bytes in front of the output payload
     constexpr uint32_t SKIP = OBF ? 0u : 8u;   // salt bytes in front of the input payload
     constexpr int U = kWU;
@@ -360,6 +368,99 @@ __global__ __launch_bounds__(kGroup* kWavesPerBlock, HY_WAVE_MIN_WAVES) void sal
                                          (uint32_t)(kr[3] >> 32));
     }
     hy_wave_sync();
+
+    if constexpr (FLAT) {
+        // ---- 3'. boundary-free sweep: every chunk is composed in the sweep from at most
+        // two datagrams, q (the one holding byte a, or the last starting before it) and
+        // q + 1.  Each contributes its salt bytes and its payload bytes, the latter from
+        // one 16-byte window inside the payload loaded with the sweep's own loads.  So
+        // no boundary window is read long before the sweep reaches its line, and every
+        // lane runs the same instructions: interior chunks simply have empty masks for
+        // q + 1.  Only chunks at run edges that are shared with another run are partial
+        // (byte-masked stores).
+        const uint32_t nchunks = (totm + 15u) >> 4;
+        constexpr int UF = HY_FLAT_U;   // chunks per lane in flight (two windows each)
+        constexpr uint32_t STEP = kGroup * UF;
+        for (uint32_t c0 = 0; c0 < nchunks; c0 += STEP) {
+            u128 va[UF], vb[UF];
+            uint32_t qv[UF];
+#pragma unroll
+            for (int u = 0; u < UF; ++u) {   // every load first
+                const uint32_t c = c0 + u * kGroup + lane, a = c << 4;
+                const uint32_t qq = group_search(G, a);
+                qv[u] = qq;
+                const uint2 owq = G.ow[qq];
+                const int pa = (int)a - (int)(owq.x + SALT), pl = (int)owq.y - (int)SALT;
+                va[u] = 0;
+                vb[u] = 0;
+                if (c < nchunks && owq.y && pa > -16 && pa < pl)
+                    va[u] = load16_nt(in + G.io[qq] + min(max(pa, 0), pl - 16));
+                if (c < nchunks && qq + 1 < cnt) {
+                    const uint2 own = G.ow[qq + 1];
+                    if (own.y && (int)(own.x + SALT) - (int)a < 16) vb[u] = load16_nt(in + G.io[qq + 1]);
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < UF; ++u) {
+                const uint32_t c = c0 + u * kGroup + lane, a = c << 4;
+                if (c >= nchunks) continue;
+                const uint32_t qq = qv[u], h = (a >> 4) & 1u;
+                const uint2 owq = G.ow[qq];
+                u128 r = 0;
+                uint32_t cov = 0;
+                bool mine = false;   // does q's region reach into the chunk
+                if (owq.y) {
+                    const int pa = (int)a - (int)(owq.x + SALT), pl = (int)owq.y - (int)SALT;
+                    const int lo = max(0, -pa), hi = min(16, pl - pa);
+                    if (lo < hi) {   // q's payload bytes
+                        const int d = min(max(pa, 0), pl - 16) - pa;
+                        const u128 X = d >= 0 ? (va[u] << (8 * d)) : (va[u] >> (8 * -d));
+                        const uint4 kk = G.key[2 * qq + h];
+                        u128 k128;
+                        __builtin_memcpy(&k128, &kk, 16);
+                        r |= (X ^ k128) & bytemask((uint32_t)lo, (uint32_t)hi);
+                        cov |= ((1u << (hi - lo)) - 1u) << lo;
+                        mine = true;
+                    }
+                    if (OBF) {   // q's salt bytes
+                        const int s0 = (int)owq.x - (int)a;
+                        const int sl = max(0, s0), sh = min(16, s0 + 8);
+                        if (sl < sh) {
+                            const u128 S = (u128)G.salt[qq];
+                            r |= (s0 >= 0 ? (S << (8 * s0)) : (S >> (8 * -s0))) & bytemask((uint32_t)sl, (uint32_t)sh);
+                            cov |= ((1u << (sh - sl)) - 1u) << sl;
+                            mine = true;
+                        }
+                    }
+                }
+                if (qq + 1 < cnt) {
+                    const uint2 own = G.ow[qq + 1];
+                    const int t0 = (int)own.x - (int)a;   // > 0: q + 1 starts after byte a
+                    if (own.y && t0 < 16) {
+                        if (OBF) {   // its salt
+                            const int sh = min(16, t0 + 8);
+                            r |= ((u128)G.salt[qq + 1] << (8 * t0)) & bytemask((uint32_t)t0, (uint32_t)sh);
+                            cov |= ((1u << (sh - t0)) - 1u) << t0;
+                        }
+                        const int lo = t0 + (int)SALT;   // its payload, from its first window
+                        if (lo < 16) {
+                            const uint4 kk = G.key[2 * (qq + 1) + h];
+                            u128 k128;
+                            __builtin_memcpy(&k128, &kk, 16);
+                            r |= ((vb[u] << (8 * lo)) ^ k128) & bytemask((uint32_t)lo, 16u);
+                            cov |= (0xFFFFu << lo) & 0xFFFFu;
+                        }
+                    }
+                }
+                uint8_t* dst = B.out + G.delta[mine ? qq : min(qq + 1, (uint32_t)kGroup - 1)] + a;
+                if (cov == 0xFFFFu)
+                    store16_stream(dst, r);
+                else if (cov)
+                    store_masked(dst, r, cov);
+            }
+        }
+        return;
+    }
 
     // ---- 3. boundary chunks datagram `lane` owns (the first datagram touching a
     // chunk owns it: exclusive max-scan of region ends) that are not inside one
@@ -533,12 +634,32 @@ inline uint32_t wave_run_log2() {
     return (uint32_t)v;
 }
 
+// The boundary-free sweep applies when every datagram of a slotted batch has the
+// same length, a region of 16 bytes or more (payload windows of 16 bytes fit) and
+// nothing is dropped: then a 16-byte chunk touches at most two regions.
+template <bool OBF>
+inline bool flat_ok(const BatchParams& b) {
+    if (b.out_stride == 0 || b.in_len || b.n == 0) return false;
+    const uint64_t L = b.len_uniform;
+    if (L > kMaxDatagram || L < (OBF ? 16u : 24u)) return false;
+    const uint64_t W = OBF ? L + 8 : L - 8;
+    if ((b.pkt_cap && W > b.pkt_cap) || W > b.out_stride) return false;
+    return (b.n - 1) * b.out_stride + W <= b.out_cap;
+}
+
 template <bool OBF, bool PACKED, int SW>
 void launch_wave_sw(const BatchParams& bp, const KeyParams& k, hipStream_t s) {
     const uint64_t ngroups = div_up(bp.n, kGroup);
     const uint64_t blocks = div_up(ngroups, kWavesPerBlock);
     BatchParams b = bp;
     b.run_log2 = PACKED ? wave_packed_run_log2() : wave_run_log2();
+    if constexpr (!PACKED) {
+        if (b.kernel == HY_KERNEL_FLAT && flat_ok<OBF>(b)) {
+            hipLaunchKernelGGL((salamander_wave_kernel<OBF, false, SW, true>), dim3((uint32_t)blocks),
+                               dim3(kGroup * kWavesPerBlock), 0, s, b, k);
+            return;
+        }
+    }
     hipLaunchKernelGGL((salamander_wave_kernel<OBF, PACKED, SW>), dim3((uint32_t)blocks),
                        dim3(kGroup * kWavesPerBlock), 0, s, b, k);
 }

@@ -136,7 +136,7 @@ class SalamanderObfuscator:
     def __exit__(self, *exc):
         self.close()
 
-    KERNELS = {"auto": 0, "wave": 1, "persistent": 2, "uniform": 3, "stream": 4, "pipe": 5}
+    KERNELS = {"auto": 0, "wave": 1, "persistent": 2, "uniform": 3, "stream": 4, "pipe": 5, "flat": 6}
 
     def set_kernel(self, kernel: str) -> None:
         """Batch kernel of this context: "auto" (per layout), "wave", "persistent", "uniform" or "stream"."""

@@ -99,9 +99,12 @@ int hyobfs_salamander_device(const hyobfs_salamander* ctx);
    4 KiB sweeps); both measure slower than AUTO on 1M x 1200 B.
    HYOBFS_KERNEL_PIPE is STREAM with the keys pass on a second stream the
    context owns (one per caller stream), each sweep chunk ordered after its keys
-   by an event, so the key grid never holds a sweep launch open.  The
-   HYOBFS_KERNEL environment variable (wave|persistent|uniform|stream|pipe)
-   overrides AUTO.  UNIFORM, STREAM or PIPE on a batch that is not uniform falls back
+   by an event, so the key grid never holds a sweep launch open.
+   HYOBFS_KERNEL_FLAT is the wave kernel with a boundary-free sweep (each chunk
+   composed from at most two datagrams in the sweep itself) for slotted batches
+   of one length (16 B or more; 24 B or more to deobfuscate) with nothing dropped.
+   The HYOBFS_KERNEL environment variable (wave|persistent|uniform|stream|pipe|flat)
+   overrides AUTO.  UNIFORM, STREAM, PIPE or FLAT on a batch that does not qualify falls back
    to the AUTO choice.  Returns HYOBFS_ERR_INVALID for an unknown value.
    Outputs are identical. */
 enum {
@@ -110,7 +113,8 @@ enum {
     HYOBFS_KERNEL_PERSISTENT = 2,
     HYOBFS_KERNEL_UNIFORM = 3,
     HYOBFS_KERNEL_STREAM = 4,
-    HYOBFS_KERNEL_PIPE = 5
+    HYOBFS_KERNEL_PIPE = 5,
+    HYOBFS_KERNEL_FLAT = 6
 };
 int hyobfs_salamander_set_kernel(hyobfs_salamander* ctx, int kernel);
 

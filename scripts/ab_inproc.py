@@ -14,7 +14,7 @@ from hysteria_amd import _lib  # noqa: E402
 
 # each argument: path/to/lib.so[:kernel[:VAR=value,...]]  (kernel = auto|wave|persistent|uniform|stream|pipe;
 # the variables are set for that variant's launches only: per-launch knobs such as HYOBFS_PERSIST_ORDER)
-KERNELS = {"auto": 0, "wave": 1, "persistent": 2, "uniform": 3, "stream": 4, "pipe": 5}
+KERNELS = {"auto": 0, "wave": 1, "persistent": 2, "uniform": 3, "stream": 4, "pipe": 5, "flat": 6}
 specs = [a.split(":") for a in (sys.argv[1:] or ["hysteria_amd/libhyobfs.so"])]
 libs = [x[0] for x in specs]
 P, L = 1 << 20, int(os.environ.get("AB_LEN", "1200"))

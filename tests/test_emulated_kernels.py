@@ -39,6 +39,7 @@ SPECS = {
     "test_emulated_stream_kernel_pipelined": lambda p: (
         "uniform", p["args"], {"HYOBFS_KERNEL": "stream", "HYEMU_CUS": "2", "HYOBFS_STREAM_FIRST_RUNS": "12",
                                "HYOBFS_STREAM_GROW": "2"}),
+    "test_emulated_flat_sweep": lambda p: (p["which"], p["args"], {"HYOBFS_KERNEL": "flat", "HYEMU_CUS": "2"}),
     "test_emulated_pipe_kernel": lambda p: (
         "uniform", p["args"], {"HYOBFS_KERNEL": "pipe", "HYEMU_CUS": "2", "HYOBFS_PIPE_FIRST_RUNS": "12",
                                "HYOBFS_PIPE_GROW": "2", "HYOBFS_PIPE_KEY_BLOCKS": "1"}),
@@ -173,6 +174,22 @@ def test_emulated_stream_kernel_pipelined(emu_lib, args):
                                     "HYOBFS_STREAM_FIRST_RUNS": "12", "HYOBFS_STREAM_GROW": "2"})
 
 
+
+
+# the wave kernel's boundary-free sweep (HYOBFS_KERNEL=flat): uniform slotted batches at
+# every chunk phase (lengths 16..24 and odd ones), run edges, the 2048-byte maximum,
+# and layouts that do not qualify (fall back to the parked sweep)
+FLAT_CASES = [c for c in UNIFORM_CASES if int(c[1].split()[0]) < 1000] + [
+    ("uniform", "300 16 1"), ("uniform", "300 17 1"), ("uniform", "300 23 1"), ("uniform", "300 24 0"),
+    ("uniform", "300 25 0"), ("uniform", "257 1203 1"), ("uniform", "257 1209 0"), ("uniform", "130 2040 1"),
+    ("uniform", "130 2048 0"), ("uniform", "300 16 0"), ("far", "200 300 15 1"), ("far", "200 300 15 0"),
+    ("ragged", "9 1500 2100 1 1"), ("ragged", "12 700 100 1 0"),
+]
+
+
+@pytest.mark.parametrize("which,args", FLAT_CASES)
+def test_emulated_flat_sweep(emu_lib, which, args):
+    _run(emu_lib, which, args, {"HYOBFS_KERNEL": "flat", "HYEMU_CUS": "2"})
 
 
 @pytest.mark.parametrize("args", ["1001 1200 0", "1000 1200 1", "999 1192 1", "64 16 1"])

@@ -17,7 +17,7 @@ pytestmark = pytest.mark.gpu
 PSK = b"average_password"
 
 
-@pytest.fixture(scope="module", params=["auto", "wave", "persistent", "uniform", "stream", "pipe"])
+@pytest.fixture(scope="module", params=["auto", "wave", "persistent", "uniform", "stream", "pipe", "flat"])
 def obfs(gpu, request):
     """One context per batch kernel: auto (the shipped per-layout choice), and
     each kernel forced on every layout (salamander_wave.h, salamander_device.h;
