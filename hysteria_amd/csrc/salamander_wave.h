@@ -36,10 +36,10 @@ constexpr int kWavesPerBlock = 4;    // independent waves per workgroup
 #endif
 constexpr int kWU = HY_WU;           // chunks per lane per sweep iteration
 #ifndef HY_FLAT_U
-#define HY_FLAT_U 4                  // the boundary-free sweep: chunks per lane per iteration
+#define HY_FLAT_U 8                  // the boundary-free sweep: chunks per lane per iteration
 #endif
 #ifndef HY_FLAT_MIN_WAVES
-#define HY_FLAT_MIN_WAVES 6          // ... and its waves per SIMD (two windows per chunk need registers)
+#define HY_FLAT_MIN_WAVES 8          // ... and its waves per SIMD
 #endif
 #ifndef HY_RUN_LOG2
 #define HY_RUN_LOG2 3
@@ -213,6 +213,17 @@ __device__ __forceinline__ u128 load16_nt(const uint8_t* p) {
 #endif
 }
 
+__device__ __forceinline__ uint64_t load8_nt(const uint8_t* p) {   // 8-aligned
+#if defined(HYOBFS_EMULATE)
+    return load8u(p);
+#else
+    typedef uint32_t v2u __attribute__((ext_vector_type(2)));
+    typedef const __attribute__((address_space(1))) v2u gv2u;
+    const v2u v = __builtin_nontemporal_load((gv2u*)(p));
+    return (uint64_t)v.y << 32 | v.x;
+#endif
+}
+
 // Last datagram of the group whose region starts at or before virtual offset a.
 __device__ __forceinline__ uint32_t group_search(const GroupBuf& G, uint32_t a) {
     uint32_t qq = 0;   // last datagram whose region starts at or before a
@@ -370,93 +381,66 @@ salamander_wave_kernel(BatchParams B, KeyParams K) {
     hy_wave_sync();
 
     if constexpr (FLAT) {
-        // ---- 3'. boundary-free sweep: every chunk is composed in the sweep from at most
-        // two datagrams, q (the one holding byte a, or the last starting before it) and
-        // q + 1.  Each contributes its salt bytes and its payload bytes, the latter from
-        // one 16-byte window inside the payload loaded with the sweep's own loads.  So
-        // no boundary window is read long before the sweep reaches its line, and every
-        // lane runs the same instructions: interior chunks simply have empty masks for
-        // q + 1.  Only chunks at run edges that are shared with another run are partial
-        // (byte-masked stores).
+        // ---- 3'. boundary-free sweep (uniform slotted batches whose lengths, slots and
+        // input offsets are multiples of 8).  Every region edge then falls on an 8-byte
+        // boundary, so each 8-byte half of a 16-byte chunk is exactly one of: a salt,
+        // 8 payload bytes of one datagram, or nothing.  The chunk's datagrams are q (the
+        // last region starting at or before it) and q + 1.  Each half is one 8-byte
+        // load (or the salt) XOR the key qword, all in the sweep's own loads: no early
+        // boundary windows, no parking, and every lane runs the same instructions.
+        // Only halves that belong to another run are left out (byte-masked store).
         const uint32_t nchunks = (totm + 15u) >> 4;
-        constexpr int UF = HY_FLAT_U;   // chunks per lane in flight (two windows each)
+        constexpr int UF = HY_FLAT_U;
         constexpr uint32_t STEP = kGroup * UF;
+        // half x of the chunk at a: class (0 none, 1 salt, 2 payload), datagram, input address
+        auto half_src = [&](uint32_t qq, uint32_t x, uint32_t& k, uint64_t& addr) -> uint32_t {
+            const uint2 owq = G.ow[qq];
+            const uint2 own = qq + 1 < cnt ? G.ow[qq + 1] : make_uint2(0u, 0u);
+            if (owq.y && x >= owq.x && x < owq.x + owq.y) {   // (x < owq.x: the chunks before the first run)
+                k = qq;
+            } else if (own.y && x >= own.x && x < own.x + own.y) {
+                k = qq + 1;
+            } else {
+                return 0u;
+            }
+            const uint32_t ox = G.ow[k].x;
+            if (OBF && x == ox) return 1u;
+            addr = G.io[k] + (x - ox - SALT);
+            return 2u;
+        };
         for (uint32_t c0 = 0; c0 < nchunks; c0 += STEP) {
-            u128 va[UF], vb[UF];
-            uint32_t qv[UF];
+            uint64_t v0[UF], v1[UF];
+            uint32_t cls[UF];   // per half: class (2 bits) | datagram (6 bits) << 2
 #pragma unroll
             for (int u = 0; u < UF; ++u) {   // every load first
                 const uint32_t c = c0 + u * kGroup + lane, a = c << 4;
-                const uint32_t qq = group_search(G, a);
-                qv[u] = qq;
-                const uint2 owq = G.ow[qq];
-                const int pa = (int)a - (int)(owq.x + SALT), pl = (int)owq.y - (int)SALT;
-                va[u] = 0;
-                vb[u] = 0;
-                if (c < nchunks && owq.y && pa > -16 && pa < pl)
-                    va[u] = load16_nt(in + G.io[qq] + min(max(pa, 0), pl - 16));
-                if (c < nchunks && qq + 1 < cnt) {
-                    const uint2 own = G.ow[qq + 1];
-                    if (own.y && (int)(own.x + SALT) - (int)a < 16) vb[u] = load16_nt(in + G.io[qq + 1]);
+                v0[u] = 0;
+                v1[u] = 0;
+                cls[u] = 0;
+                if (c < nchunks) {
+                    const uint32_t qq = group_search(G, a);
+                    uint32_t k0 = 0, k1 = 0;
+                    uint64_t a0 = 0, a1 = 0;
+                    const uint32_t c0s = half_src(qq, a, k0, a0), c1s = half_src(qq, a + 8, k1, a1);
+                    if (c0s == 2u) v0[u] = load8_nt(in + a0);
+                    if (c1s == 2u) v1[u] = load8_nt(in + a1);
+                    cls[u] = c0s | k0 << 2 | c1s << 8 | k1 << 10;
                 }
             }
 #pragma unroll
             for (int u = 0; u < UF; ++u) {
-                const uint32_t c = c0 + u * kGroup + lane, a = c << 4;
-                if (c >= nchunks) continue;
-                const uint32_t qq = qv[u], h = (a >> 4) & 1u;
-                const uint2 owq = G.ow[qq];
-                u128 r = 0;
-                uint32_t cov = 0;
-                bool mine = false;   // does q's region reach into the chunk
-                if (owq.y) {
-                    const int pa = (int)a - (int)(owq.x + SALT), pl = (int)owq.y - (int)SALT;
-                    const int lo = max(0, -pa), hi = min(16, pl - pa);
-                    if (lo < hi) {   // q's payload bytes
-                        const int d = min(max(pa, 0), pl - 16) - pa;
-                        const u128 X = d >= 0 ? (va[u] << (8 * d)) : (va[u] >> (8 * -d));
-                        const uint4 kk = G.key[2 * qq + h];
-                        u128 k128;
-                        __builtin_memcpy(&k128, &kk, 16);
-                        r |= (X ^ k128) & bytemask((uint32_t)lo, (uint32_t)hi);
-                        cov |= ((1u << (hi - lo)) - 1u) << lo;
-                        mine = true;
-                    }
-                    if (OBF) {   // q's salt bytes
-                        const int s0 = (int)owq.x - (int)a;
-                        const int sl = max(0, s0), sh = min(16, s0 + 8);
-                        if (sl < sh) {
-                            const u128 S = (u128)G.salt[qq];
-                            r |= (s0 >= 0 ? (S << (8 * s0)) : (S >> (8 * -s0))) & bytemask((uint32_t)sl, (uint32_t)sh);
-                            cov |= ((1u << (sh - sl)) - 1u) << sl;
-                            mine = true;
-                        }
-                    }
-                }
-                if (qq + 1 < cnt) {
-                    const uint2 own = G.ow[qq + 1];
-                    const int t0 = (int)own.x - (int)a;   // > 0: q + 1 starts after byte a
-                    if (own.y && t0 < 16) {
-                        if (OBF) {   // its salt
-                            const int sh = min(16, t0 + 8);
-                            r |= ((u128)G.salt[qq + 1] << (8 * t0)) & bytemask((uint32_t)t0, (uint32_t)sh);
-                            cov |= ((1u << (sh - t0)) - 1u) << t0;
-                        }
-                        const int lo = t0 + (int)SALT;   // its payload, from its first window
-                        if (lo < 16) {
-                            const uint4 kk = G.key[2 * (qq + 1) + h];
-                            u128 k128;
-                            __builtin_memcpy(&k128, &kk, 16);
-                            r |= ((vb[u] << (8 * lo)) ^ k128) & bytemask((uint32_t)lo, 16u);
-                            cov |= (0xFFFFu << lo) & 0xFFFFu;
-                        }
-                    }
-                }
-                uint8_t* dst = B.out + G.delta[mine ? qq : min(qq + 1, (uint32_t)kGroup - 1)] + a;
-                if (cov == 0xFFFFu)
-                    store16_stream(dst, r);
-                else if (cov)
-                    store_masked(dst, r, cov);
+                const uint32_t c = c0 + u * kGroup + lane, a = c << 4, h = (a >> 4) & 1u;
+                const uint32_t c0s = cls[u] & 3u, k0 = (cls[u] >> 2) & 63u;
+                const uint32_t c1s = (cls[u] >> 8) & 3u, k1 = (cls[u] >> 10) & 63u;
+                if (!c0s && !c1s) continue;
+                const uint4 kk0 = G.key[2 * k0 + h], kk1 = G.key[2 * k1 + h];
+                const uint64_t lo = c0s == 2u ? v0[u] ^ ((uint64_t)kk0.y << 32 | kk0.x) : OBF ? G.salt[k0] : 0ull;
+                const uint64_t hi = c1s == 2u ? v1[u] ^ ((uint64_t)kk1.w << 32 | kk1.z) : OBF ? G.salt[k1] : 0ull;
+                uint8_t* dst = B.out + G.delta[c0s ? k0 : k1] + a;
+                if (c0s && c1s)
+                    store16_stream(dst, (u128)hi << 64 | lo);
+                else
+                    store_masked(dst, (u128)hi << 64 | lo, c0s ? 0x00FFu : 0xFF00u);
             }
         }
         return;
@@ -635,13 +619,16 @@ inline uint32_t wave_run_log2() {
 }
 
 // The boundary-free sweep applies when every datagram of a slotted batch has the
-// same length, a region of 16 bytes or more (payload windows of 16 bytes fit) and
-// nothing is dropped: then a 16-byte chunk touches at most two regions.
+// same length (a multiple of 8, like the slot stride and the input stride), a
+// region of 16 bytes or more, and nothing is dropped: then a 16-byte chunk touches
+// at most two regions and splits between them at its middle if at all.
 template <bool OBF>
 inline bool flat_ok(const BatchParams& b) {
-    if (b.out_stride == 0 || b.in_len || b.n == 0) return false;
+    if (b.out_stride == 0 || b.in_len || b.in_off || b.n == 0) return false;
     const uint64_t L = b.len_uniform;
     if (L > kMaxDatagram || L < (OBF ? 16u : 24u)) return false;
+    // every region edge and input qword on an 8-byte boundary
+    if ((L | b.out_stride | b.in_stride | reinterpret_cast<uintptr_t>(b.in)) & 7u) return false;
     const uint64_t W = OBF ? L + 8 : L - 8;
     if ((b.pkt_cap && W > b.pkt_cap) || W > b.out_stride) return false;
     return (b.n - 1) * b.out_stride + W <= b.out_cap;

@@ -182,7 +182,7 @@ def test_emulated_stream_kernel_pipelined(emu_lib, args):
 FLAT_CASES = [c for c in UNIFORM_CASES if int(c[1].split()[0]) < 1000] + [
     ("uniform", "300 16 1"), ("uniform", "300 17 1"), ("uniform", "300 23 1"), ("uniform", "300 24 0"),
     ("uniform", "300 25 0"), ("uniform", "257 1203 1"), ("uniform", "257 1209 0"), ("uniform", "130 2040 1"),
-    ("uniform", "130 2048 0"), ("uniform", "300 16 0"), ("far", "200 300 15 1"), ("far", "200 300 15 0"),
+    ("uniform", "130 2048 0"), ("uniform", "300 16 0"), ("far", "200 296 15 1"), ("far", "200 296 15 0"),
     ("ragged", "9 1500 2100 1 1"), ("ragged", "12 700 100 1 0"),
 ]
 
