@@ -422,8 +422,14 @@ salamander_wave_kernel(BatchParams B, KeyParams K) {
                     uint32_t k0 = 0, k1 = 0;
                     uint64_t a0 = 0, a1 = 0;
                     const uint32_t c0s = half_src(qq, a, k0, a0), c1s = half_src(qq, a + 8, k1, a1);
-                    if (c0s == 2u) v0[u] = load8_nt(in + a0);
-                    if (c1s == 2u) v1[u] = load8_nt(in + a1);
+                    if (c0s == 2u && c1s == 2u && k0 == k1) {   // inside one payload: one 16-byte load
+                        const u128 x = load16_nt(in + a0);
+                        v0[u] = (uint64_t)x;
+                        v1[u] = (uint64_t)(x >> 64);
+                    } else {
+                        if (c0s == 2u) v0[u] = load8_nt(in + a0);
+                        if (c1s == 2u) v1[u] = load8_nt(in + a1);
+                    }
                     cls[u] = c0s | k0 << 2 | c1s << 8 | k1 << 10;
                 }
             }
