@@ -328,12 +328,17 @@ int run_batch(hyobfs_salamander* c, const hyobfs_batch* b, void* stream, bool ob
         if (need > keys_off) bp.keys = reinterpret_cast<uint64_t*>(w + keys_off);
         if (bp.keys && hyobfs::resolve_kernel(c->kernel) == HYOBFS_KERNEL_PIPE) {
             if (!e->side.s) {   // the side lane of this caller stream, kept until the context is freed
-                if (hipStreamCreateWithFlags(&e->side.s, hipStreamNonBlocking) != hipSuccess) {
-                    e->side.s = nullptr;
+                hyobfs::SideLane sl;
+                bool ok = hipStreamCreateWithFlags(&sl.s, hipStreamNonBlocking) == hipSuccess;
+                for (auto& ev : sl.ev)
+                    ok = ok && hipEventCreateWithFlags(&ev, hipEventDisableTiming) == hipSuccess;
+                if (!ok) {   // nothing half-made stays behind: the next call tries again
+                    for (auto& ev : sl.ev)
+                        if (ev) (void)hipEventDestroy(ev);
+                    if (sl.s) (void)hipStreamDestroy(sl.s);
                     return HYOBFS_ERR_HIP;
                 }
-                for (auto& ev : e->side.ev)
-                    if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return HYOBFS_ERR_HIP;
+                e->side = sl;
             }
             side = &e->side;
         }
