@@ -51,17 +51,23 @@ constexpr int kWU = HY_WU;           // chunks per lane per sweep iteration
 #define HY_WAVE_MIN_WAVES 8          // __launch_bounds__ min waves per SIMD
 #endif
 
-struct GroupBuf {                    // one wave's group, in LDS (4736 B: 8 workgroups per CU)
+#ifndef HY_PACKED_PARK_SLOTS
+#define HY_PACKED_PARK_SLOTS 64      // park slots per group, packed layout (ragged mixes have more edges)
+#endif
+template <bool PACKED>
+struct GroupBufT {                   // one wave's group, in LDS (4736 B with 64 slots: 8 workgroups per CU)
+    static constexpr int kSlots = PACKED ? HY_PACKED_PARK_SLOTS : kGroup;
     uint2 ow[kGroup];                // output region start (virtual), width (0 = dropped)
     uint64_t io[kGroup];             // input payload start (absolute byte offset)
     uint64_t delta[kGroup];          // real output offset - virtual offset (the run's)
     uint4 key[2 * kGroup];           // key rotated to the output's 32-byte phase, 2 halves
     union {
         uint64_t salt[kGroup];       // salts (obfuscate), read while boundary chunks are built
-        u128 bnd[kGroup];            // then: parked boundary chunks, XORed with the owner's key half
+        u128 bnd[kSlots];            // then: parked boundary chunks, XORed with the owner's key half
     };
     uint16_t park[kGroup];           // bits 0-2 parked (first, second, last chunk), 3-5 late, 8-15 first slot
 };
+static_assert(HY_PACKED_PARK_SLOTS >= kGroup && HY_PACKED_PARK_SLOTS <= 255, "park slot index is 8 bits");
 
 // ---- BLAKE2b message words of the device block(s).  The message is
 // PSK || salt, zero padded: every word after the salt's is a compile-time 0,
@@ -143,7 +149,7 @@ __device__ __forceinline__ void wave_key(const KeyParams& K, uint64_t salt, uint
 }
 
 // All bytes datagram k of the group contributes to the 16-byte chunk at relative a.
-template <bool OBF, class SaltOf>
+template <bool OBF, class GroupBuf, class SaltOf>
 __device__ __forceinline__ void group_contrib(const GroupBuf& G, const uint8_t* __restrict__ in, uint32_t k,
                                               uint32_t a, u128& r, uint32_t& cov, SaltOf salt_of) {
     constexpr uint32_t SALT = OBF ? 8u : 0u;
@@ -225,6 +231,7 @@ __device__ __forceinline__ uint64_t load8_nt(const uint8_t* p) {   // 8-aligned
 }
 
 // Last datagram of the group whose region starts at or before virtual offset a.
+template <class GroupBuf>
 __device__ __forceinline__ uint32_t group_search(const GroupBuf& G, uint32_t a) {
     uint32_t qq = 0;   // last datagram whose region starts at or before a
 #pragma unroll
@@ -235,6 +242,7 @@ __device__ __forceinline__ uint32_t group_search(const GroupBuf& G, uint32_t a) 
 // Where the sweep looks for a parked chunk at virtual offset a: datagram qq
 // (group_search(a), region owq) if its region reaches into the chunk, else
 // datagram qq + 1.  Returns that datagram's region in owo (width 0: none).
+template <class GroupBuf>
 __device__ __forceinline__ uint32_t park_owner(const GroupBuf& G, uint32_t a, uint32_t qq, uint2 owq, uint2& owo) {
     if (owq.y != 0 && owq.x + owq.y > a) {
         owo = owq;
@@ -260,6 +268,7 @@ salamander_wave_kernel(BatchParams B, KeyParams K) {
     constexpr uint32_t SALT = OBF ? 8u : 0u;   // salt bytes in front of the output payload
     constexpr uint32_t SKIP = OBF ? 0u : 8u;   // salt bytes in front of the input payload
     constexpr int U = kWU;
+    using GroupBuf = GroupBufT<PACKED>;
     __shared__ GroupBuf gbuf[kWavesPerBlock];
 
     const int lane = threadIdx.x & 63;
@@ -495,7 +504,7 @@ salamander_wave_kernel(BatchParams B, KeyParams K) {
 #endif
         const uint32_t np = (uint32_t)__builtin_popcount(parkm);
         const uint32_t base = (uint32_t)wave_incl_scan(np, lane) - np;
-        if (base + np > (uint32_t)kGroup) parkm = 0;   // out of slots: store late
+        if (base + np > (uint32_t)GroupBuf::kSlots) parkm = 0;   // out of slots: store late
         hy_wave_sync();   // every lane has read the salts the slots overwrite
         uint32_t sl = base;
 #pragma unroll
