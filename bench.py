@@ -49,9 +49,9 @@ KERNEL_NAMES = {
                 "stream": "keys pass + salamander_stream_kernel<obfuscate> (salamander_stream.h)",
                 "wave": "salamander_wave_kernel<obfuscate, slotted> (salamander_wave.h)",
                 "persistent": "salamander_kernel<obfuscate, slotted> (salamander_device.h)"},
-    "bimodal": {"auto": "salamander_kernel<obfuscate, packed> (salamander_device.h) + tile-sum scan",
-                "uniform": "salamander_kernel<obfuscate, packed> (salamander_device.h) + tile-sum scan",
-                "stream": "salamander_kernel<obfuscate, packed> (salamander_device.h) + tile-sum scan",
+    "bimodal": {"auto": "salamander_wave_kernel<obfuscate, packed> (salamander_wave.h) + tile-sum scan",
+                "uniform": "salamander_wave_kernel<obfuscate, packed> (salamander_wave.h) + tile-sum scan",
+                "stream": "salamander_wave_kernel<obfuscate, packed> (salamander_wave.h) + tile-sum scan",
                 "wave": "salamander_wave_kernel<obfuscate, packed> (salamander_wave.h) + tile-sum scan",
                 "persistent": "salamander_kernel<obfuscate, packed> (salamander_device.h) + tile-sum scan"},
 }

@@ -158,10 +158,9 @@ __global__ void synth_bimodal_kernel(uint32_t* dst, uint64_t n, uint64_t seed, u
 
 // ------------------------------------------------------------------ launchers
 
-// Kernel choice per layout ("Kernels"): slotted batches run the
-// wave-group kernel (salamander_wave.h), packed batches the persistent
-// workgroup kernel (salamander_device.h), which handles the boundary-heavy
-// ragged mixes better.  HYOBFS_KERNEL=wave|persistent forces one.
+// Kernel choice ("Kernels"): every batch runs the wave-group kernel
+// (salamander_wave.h) unless the persistent workgroup kernel
+// (salamander_device.h) is asked for.  HYOBFS_KERNEL=wave|persistent|... forces one.
 static int kernel_override() {   // HYOBFS_KERNEL, as HYOBFS_KERNEL_* (0 = auto)
     static int v = -1;
     if (v == -1) {
@@ -185,8 +184,9 @@ int resolve_kernel(int ctx_kernel) { return ctx_kernel ? ctx_kernel : kernel_ove
 template <bool OBF, bool PACKED>
 static void launch_main(const BatchParams& bp, const KeyParams& k, hipStream_t s) {
     const int kc = kernel_choice(bp);
-    const int ov = (kc == 1 || kc == HY_KERNEL_FLAT) ? 1 : kc == 2 ? 0 : -1;   // uniform / auto: per layout
-    const bool wave = ov >= 0 ? ov == 1 : !PACKED;
+    // auto: the wave-group kernel for both layouts (round 2: with 128 park slots per
+    // group it beats the persistent kernel on the bimodal mix)
+    const bool wave = kc != 2;
     BatchParams b = bp;
     b.kernel = kc;   // resolved (context or HYOBFS_KERNEL): the wave launcher picks its sweep from it
     switch (k.salt_pos >> 3) {

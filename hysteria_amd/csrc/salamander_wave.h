@@ -52,7 +52,9 @@ constexpr int kWU = HY_WU;           // chunks per lane per sweep iteration
 #endif
 
 #ifndef HY_PACKED_PARK_SLOTS
-#define HY_PACKED_PARK_SLOTS 64      // park slots per group, packed layout (ragged mixes have more edges)
+#define HY_PACKED_PARK_SLOTS 128     // park slots per group, packed layout: ragged mixes have up to ~2
+                                     // boundary chunks per datagram (64 slots overflowed into byte-masked
+                                     // late stores; profiles/r02_ab_packed_park_slots.txt)
 #endif
 template <bool PACKED>
 struct GroupBufT {                   // one wave's group, in LDS (4736 B with 64 slots: 8 workgroups per CU)

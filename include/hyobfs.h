@@ -90,8 +90,9 @@ void hyobfs_salamander_free(hyobfs_salamander* ctx);
 int hyobfs_salamander_device(const hyobfs_salamander* ctx);
 
 /* Batch kernel of this context (no reference counterpart: a tuning knob).
-   HYOBFS_KERNEL_AUTO picks per layout: slotted batches -> wave-group kernel,
-   packed batches -> persistent kernel.  For uniform batches (equal lengths, a
+   HYOBFS_KERNEL_AUTO picks the wave-group kernel for slotted and packed
+   batches (HYOBFS_KERNEL_PERSISTENT forces the persistent workgroup kernel,
+   the packed default until round 2).  For uniform batches (equal lengths, a
    multiple of 8, payloads of 512 B or more, dense 16-aligned input and
    output, nothing dropped) two more kernels can be asked for:
    HYOBFS_KERNEL_UNIFORM (aligned-load sweep over runs of two datagrams) and
