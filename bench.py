@@ -47,11 +47,15 @@ KERNEL_NAMES = {
     "uniform": {"auto": "salamander_wave_kernel<obfuscate, slotted> (salamander_wave.h)",
                 "uniform": "salamander_uniform_kernel<obfuscate> (salamander_uniform.h)",
                 "stream": "keys pass + salamander_stream_kernel<obfuscate> (salamander_stream.h)",
+                "pipe": "side-stream keys pass + salamander_stream_kernel<obfuscate> (salamander_stream.h)",
+                "flat": "salamander_wave_kernel<obfuscate, slotted, flat sweep> (salamander_wave.h)",
                 "wave": "salamander_wave_kernel<obfuscate, slotted> (salamander_wave.h)",
                 "persistent": "salamander_kernel<obfuscate, slotted> (salamander_device.h)"},
     "bimodal": {"auto": "salamander_wave_kernel<obfuscate, packed> (salamander_wave.h) + tile-sum scan",
                 "uniform": "salamander_wave_kernel<obfuscate, packed> (salamander_wave.h) + tile-sum scan",
                 "stream": "salamander_wave_kernel<obfuscate, packed> (salamander_wave.h) + tile-sum scan",
+                "pipe": "salamander_wave_kernel<obfuscate, packed> (salamander_wave.h) + tile-sum scan",
+                "flat": "salamander_wave_kernel<obfuscate, packed> (salamander_wave.h) + tile-sum scan",
                 "wave": "salamander_wave_kernel<obfuscate, packed> (salamander_wave.h) + tile-sum scan",
                 "persistent": "salamander_kernel<obfuscate, packed> (salamander_device.h) + tile-sum scan"},
 }
@@ -69,7 +73,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--no-bimodal", action="store_true", help="N=1: skip the configs[2] sub-object")
-    ap.add_argument("--kernel", choices=["auto", "wave", "persistent", "uniform", "stream"], default="auto")
+    ap.add_argument("--kernel", choices=["auto", "wave", "persistent", "uniform", "stream", "pipe", "flat"],
+                    default="auto")
     return ap.parse_args()
 
 

@@ -139,7 +139,8 @@ class SalamanderObfuscator:
     KERNELS = {"auto": 0, "wave": 1, "persistent": 2, "uniform": 3, "stream": 4, "pipe": 5, "flat": 6}
 
     def set_kernel(self, kernel: str) -> None:
-        """Batch kernel of this context: "auto" (per layout), "wave", "persistent", "uniform" or "stream"."""
+        """Batch kernel of this context: "auto" (the wave-group kernel), "wave", "persistent", "uniform",
+        "stream", "pipe" or "flat" (include/hyobfs.h, HYOBFS_KERNEL_*)."""
         check(self._lib.hyobfs_salamander_set_kernel(self._h, self.KERNELS[kernel]), "set_kernel")
 
     # ------------------------------------------------------------ salt source
