@@ -614,17 +614,13 @@ salamander_wave_kernel(BatchParams B, KeyParams K) {
 // ~630 MB window, tools/region_copy.hip), large enough that few 128-byte
 // lines are shared between runs of different waves.
 #ifndef HY_PACKED_RUN_LOG2
-#define HY_PACKED_RUN_LOG2 6          // packed obfuscate: one run per group
+#define HY_PACKED_RUN_LOG2 6
 #endif
-#ifndef HY_PACKED_DEOBF_RUN_LOG2
-#define HY_PACKED_DEOBF_RUN_LOG2 4    // packed deobfuscate: runs of 16 (bimodal 1.308 vs 1.392 ms,
-#endif                                // profiles/r02_ab_packed_slots_runs.txt)
-template <bool OBF>
-inline uint32_t wave_packed_run_log2() {   // packed layout: datagrams per run (HYOBFS_PACKED_RUN_LOG2 overrides both)
+inline uint32_t wave_packed_run_log2() {   // packed layout: datagrams per run (HYOBFS_PACKED_RUN_LOG2)
     static int v = -1;
     if (v < 0) {
         const char* e = std::getenv("HYOBFS_PACKED_RUN_LOG2");
-        v = e ? std::atoi(e) : OBF ? HY_PACKED_RUN_LOG2 : HY_PACKED_DEOBF_RUN_LOG2;
+        v = e ? std::atoi(e) : HY_PACKED_RUN_LOG2;
         v = v < 0 ? 0 : v > 6 ? 6 : v;
     }
     return (uint32_t)v;
@@ -660,7 +656,7 @@ void launch_wave_sw(const BatchParams& bp, const KeyParams& k, hipStream_t s) {
     const uint64_t ngroups = div_up(bp.n, kGroup);
     const uint64_t blocks = div_up(ngroups, kWavesPerBlock);
     BatchParams b = bp;
-    b.run_log2 = PACKED ? wave_packed_run_log2<OBF>() : wave_run_log2();
+    b.run_log2 = PACKED ? wave_packed_run_log2() : wave_run_log2();
     if constexpr (!PACKED) {
         if (b.kernel == HY_KERNEL_FLAT && flat_ok<OBF>(b)) {
             hipLaunchKernelGGL((salamander_wave_kernel<OBF, false, SW, true>), dim3((uint32_t)blocks),
