@@ -44,20 +44,12 @@ PSK = b"average_password"
 METRIC = "device-resident packet-obfs GiB/s @ 1200B datagrams, 1/2/4/8 MI355X"
 # the obfuscate kernel each workload runs, per --kernel (rocprof names in profiles/)
 KERNEL_NAMES = {
-    "uniform": {"auto": "salamander_wave_kernel<obfuscate, slotted> (salamander_wave.h)",
-                "uniform": "salamander_uniform_kernel<obfuscate> (salamander_uniform.h)",
-                "stream": "keys pass + salamander_stream_kernel<obfuscate> (salamander_stream.h)",
-                "pipe": "side-stream keys pass + salamander_stream_kernel<obfuscate> (salamander_stream.h)",
-                "flat": "salamander_wave_kernel<obfuscate, slotted, flat sweep> (salamander_wave.h)",
-                "wave": "salamander_wave_kernel<obfuscate, slotted> (salamander_wave.h)",
-                "persistent": "salamander_kernel<obfuscate, slotted> (salamander_device.h)"},
+    "uniform": {"auto": "salamander_tile_kernel<obfuscate> (salamander_tile.h)",
+                "tile": "salamander_tile_kernel<obfuscate> (salamander_tile.h)",
+                "wave": "salamander_wave_kernel<obfuscate, slotted> (salamander_wave.h)"},
     "bimodal": {"auto": "salamander_wave_kernel<obfuscate, packed> (salamander_wave.h) + tile-sum scan",
-                "uniform": "salamander_wave_kernel<obfuscate, packed> (salamander_wave.h) + tile-sum scan",
-                "stream": "salamander_wave_kernel<obfuscate, packed> (salamander_wave.h) + tile-sum scan",
-                "pipe": "salamander_wave_kernel<obfuscate, packed> (salamander_wave.h) + tile-sum scan",
-                "flat": "salamander_wave_kernel<obfuscate, packed> (salamander_wave.h) + tile-sum scan",
-                "wave": "salamander_wave_kernel<obfuscate, packed> (salamander_wave.h) + tile-sum scan",
-                "persistent": "salamander_kernel<obfuscate, packed> (salamander_device.h) + tile-sum scan"},
+                "tile": "salamander_wave_kernel<obfuscate, packed> (salamander_wave.h) + tile-sum scan",
+                "wave": "salamander_wave_kernel<obfuscate, packed> (salamander_wave.h) + tile-sum scan"},
 }
 
 
@@ -73,8 +65,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--no-bimodal", action="store_true", help="N=1: skip the configs[2] sub-object")
-    ap.add_argument("--kernel", choices=["auto", "wave", "persistent", "uniform", "stream", "pipe", "flat"],
-                    default="auto")
+    ap.add_argument("--kernel", choices=["auto", "wave", "tile"], default="auto")
     return ap.parse_args()
 
 

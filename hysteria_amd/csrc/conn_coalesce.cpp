@@ -10,13 +10,19 @@
 //     when it is full or max_wait_us after its first datagram, obfuscates it on
 //     the GPU (pinned staging, hyobfs_salamander_obfuscate_host) and sends it
 //     with sendmmsg, while the next batch fills.  Like a UDP sendto, the call
-//     returns once the datagram is queued; a later send failure is counted, not
-//     reported to that caller.
+//     returns once the datagram is queued.  A later send failure is counted and
+//     its errno is returned by the NEXT WriteTo on the connection (-1, that
+//     datagram not accepted): the reference returns it to the caller whose
+//     datagram failed (conn.go:93-98), which a queued send cannot do.
 //   * receive: a reader thread receives up to max_batch datagrams with
 //     recvmmsg, deobfuscates them in one GPU batch and queues the batch;
 //     ReadFrom takes the next datagram from the queue.  Datagrams that do not
 //     deobfuscate are dropped and an empty datagram is a 0-byte read, as in
-//     ReadFrom (conn.go:77-86).  The socket's SO_RCVTIMEO bounds the wait.
+//     ReadFrom (conn.go:77-86).  The socket's SO_RCVTIMEO bounds the wait (one
+//     absolute deadline per call, like SetReadDeadline).
+//   * shutdown: stop() sends what was accepted, wakes every caller blocked in
+//     ReadFrom / WriteTo (they return -1, EBADF) and joins the threads; the
+//     memory is freed only once no caller is left inside.
 #include "conn_coalesce.h"
 
 #include <errno.h>
@@ -113,6 +119,7 @@ struct Coalescer {
     std::mutex tx_mu;                    // waits: flusher for datagrams, writers for space
     std::condition_variable cv_flush, cv_space;
     std::atomic<uint64_t> accepted{0}, sent{0}, tx_batches{0}, tx_errors{0};
+    std::atomic<int> tx_err_pending{0};  // errno of the first failed send not yet reported
     std::thread flusher;
     // receive
     Batch rx[3];
@@ -122,6 +129,8 @@ struct Coalescer {
     int rx_err = 0;
     std::atomic<uint64_t> received{0}, rx_batches{0}, rx_dropped{0};
     std::thread reader;
+    std::atomic<int> callers{0};         // threads inside coalescer_read / coalescer_write
+    bool stopped = false;
 
     bool has_space() const { return !tx[cur].sealed && tx[cur].count < max_batch; }
     void flush_loop();
@@ -143,6 +152,8 @@ void Coalescer::send_batch(Batch& b, uint32_t n) {
     d.out_len = b.b.olen;
     if (hyobfs_salamander_obfuscate_host(ctx, &d, 0) != HYOBFS_OK) {
         tx_errors += n;
+        int z = 0;
+        tx_err_pending.compare_exchange_strong(z, EIO);
         sent += n;   // handled (lost): flush() must not wait for them
         return;
     }
@@ -168,7 +179,9 @@ void Coalescer::send_batch(Batch& b, uint32_t n) {
             (void)poll(&pf, 1, 10);
             continue;
         }
-        ++tx_errors;   // this datagram cannot be sent (e.g. no route): skip it
+        ++tx_errors;   // this datagram cannot be sent (e.g. no route): skip it, report it to the next WriteTo
+        int z = 0;
+        tx_err_pending.compare_exchange_strong(z, errno ? errno : EIO);
         ++done;
     }
     sent += n;
@@ -248,8 +261,15 @@ void Coalescer::read_loop() {
             k = recvmmsg(fd, b.msg.data(), max_batch, MSG_DONTWAIT, nullptr);
             if (k > 0) break;
             if (k < 0 && errno != EAGAIN && errno != EWOULDBLOCK && errno != EINTR) {
-                std::lock_guard<std::mutex> lk(rx_mu);
-                rx_err = errno;   // reported by ReadFrom once the queue is empty
+                const int e = errno;
+                std::unique_lock<std::mutex> lk(rx_mu);
+                rx_err = e;   // reported by ReadFrom once the queue is empty
+                cv_ready.notify_all();
+                // the socket is gone (closed under us): park until stop instead of
+                // spinning on POLLNVAL; other errors back off briefly
+                const bool fatal = e == EBADF || e == ENOTSOCK || e == EINVAL || e == EFAULT;
+                cv_free.wait_for(lk, fatal ? std::chrono::hours(24) : std::chrono::milliseconds(1),
+                                 [&] { return stop.load(); });
                 break;
             }
         }
@@ -310,8 +330,8 @@ Coalescer* coalescer_new(int fd, hyobfs_salamander* ctx, uint32_t max_batch, uin
     return q;
 }
 
-void coalescer_free(Coalescer* q) {
-    if (!q) return;
+void coalescer_stop(Coalescer* q) {
+    if (!q || q->stopped) return;
     {
         std::lock_guard<std::mutex> a(q->tx_mu);
         std::lock_guard<std::mutex> b(q->rx_mu);
@@ -323,15 +343,48 @@ void coalescer_free(Coalescer* q) {
     q->cv_ready.notify_all();
     q->flusher.join();   // sends what was accepted first
     q->reader.join();
+    q->stopped = true;
+}
+
+void coalescer_free(Coalescer* q) {
+    if (!q) return;
+    coalescer_stop(q);
+    // callers woken by stop leave through the mutexes and condition variables
+    // of q: free it only once the last one is out
+    while (q->callers.load(std::memory_order_acquire) > 0) {
+        q->cv_space.notify_all();
+        q->cv_ready.notify_all();
+        std::this_thread::yield();
+    }
     for (auto& b : q->tx) b.b.release();
     for (auto& b : q->rx) b.b.release();
     delete q;
 }
 
+namespace {
+struct CallerGuard {   // counts a caller inside the coalescer (see coalescer_free)
+    Coalescer* q;
+    explicit CallerGuard(Coalescer* c) : q(c) { q->callers.fetch_add(1, std::memory_order_acq_rel); }
+    ~CallerGuard() { q->callers.fetch_sub(1, std::memory_order_acq_rel); }
+};
+}  // namespace
+
 int64_t coalescer_write(Coalescer* q, const uint8_t* p, size_t len, const void* addr, uint32_t addrlen) {
+    CallerGuard g(q);
     if (addrlen > sizeof(sockaddr_storage)) {
         errno = EINVAL;
         return -1;
+    }
+    if (q->stop) {
+        errno = EBADF;
+        return -1;
+    }
+    if (q->tx_err_pending.load(std::memory_order_relaxed)) {   // an earlier datagram's send failed
+        const int e = q->tx_err_pending.exchange(0);
+        if (e) {
+            errno = e;
+            return -1;
+        }
     }
     Batch* b;
     uint32_t idx;
@@ -375,6 +428,14 @@ int64_t coalescer_write(Coalescer* q, const uint8_t* p, size_t len, const void* 
 }
 
 int64_t coalescer_read(Coalescer* q, uint8_t* p, size_t cap, void* addr, uint32_t* addrlen) {
+    CallerGuard g(q);
+    // SetReadDeadline: SO_RCVTIMEO read once, one absolute deadline for the whole call
+    timeval tv{0, 0};
+    socklen_t tl = sizeof tv;
+    (void)getsockopt(q->fd, SOL_SOCKET, SO_RCVTIMEO, &tv, &tl);
+    const auto t = std::chrono::seconds(tv.tv_sec) + std::chrono::microseconds(tv.tv_usec);
+    const bool timed = t.count() != 0;
+    const Clock::time_point deadline = Clock::now() + t;
     for (;;) {
         int bi;
         uint32_t idx;
@@ -390,13 +451,10 @@ int64_t coalescer_read(Coalescer* q, uint8_t* p, size_t cap, void* addr, uint32_
                     errno = EBADF;
                     return -1;
                 }
-                timeval tv{0, 0};
-                socklen_t tl = sizeof tv;
-                (void)getsockopt(q->fd, SOL_SOCKET, SO_RCVTIMEO, &tv, &tl);   // SetReadDeadline
-                const auto t = std::chrono::seconds(tv.tv_sec) + std::chrono::microseconds(tv.tv_usec);
-                if (t.count() == 0) {
+                if (!timed) {
                     q->cv_ready.wait(lk);
-                } else if (!q->cv_ready.wait_for(lk, t, [&] { return !q->ready.empty() || q->rx_err || q->stop; })) {
+                } else if (!q->cv_ready.wait_until(lk, deadline,
+                                                   [&] { return !q->ready.empty() || q->rx_err || q->stop; })) {
                     errno = EAGAIN;
                     return -1;
                 }

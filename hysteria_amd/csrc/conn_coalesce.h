@@ -13,9 +13,12 @@ struct Coalescer;
 
 // Starts the flusher and reader threads on fd.  nullptr on allocation failure.
 Coalescer* coalescer_new(int fd, hyobfs_salamander* ctx, uint32_t max_batch, uint32_t max_wait_us);
-// Sends what was accepted, stops the threads, frees everything (not the fd).
+// Sends what was accepted, wakes blocked callers (-1, EBADF), stops the threads.
+void coalescer_stop(Coalescer* q);
+// coalescer_stop, then frees everything (not the fd) once no caller is inside.
 void coalescer_free(Coalescer* q);
-// WriteTo: accepted datagrams return len (also > 2040: the empty-datagram quirk).
+// WriteTo: accepted datagrams return len (also > 2040: the empty-datagram quirk);
+// -1 with the errno of an earlier datagram whose send failed (reported once).
 int64_t coalescer_write(Coalescer* q, const uint8_t* p, size_t len, const void* addr, uint32_t addrlen);
 // ReadFrom: bytes written to p, or -1 with errno (EAGAIN on the socket's receive timeout).
 int64_t coalescer_read(Coalescer* q, uint8_t* p, size_t cap, void* addr, uint32_t* addrlen);

@@ -38,18 +38,12 @@ struct hyobfs_salamander {
     uint8_t* stage = nullptr;
     uint8_t* stage_dev = nullptr;
     size_t stage_cap = 0;       // bytes for each of in and out
-    // context-owned packed-batch scratch, one buffer per stream (a buffer is only
-    // ever used by launches on its own stream, so stream order protects it).
-    // ws_mu is held from the lookup through the kernel launch, so a growing call
-    // can synchronise that stream and free the old buffer safely.
-    struct StreamWs {
-        hipStream_t s = nullptr;
-        void* p = nullptr;
-        uint64_t cap = 0;
-        hyobfs::SideLane side;   // HYOBFS_KERNEL_PIPE: key-pass stream + events, made on first use
-    };
-    std::vector<StreamWs> ws;
-    std::mutex ws_mu;
+    // packed batches without a caller workspace: tile-sum scratch allocated
+    // stream-ordered from this context-owned pool and freed behind the launch
+    // on the same stream, so any number of caller streams (and threads) share
+    // it and device memory stays bounded (release threshold below)
+    hipMemPool_t pool = nullptr;
+    std::mutex pool_mu;          // creation only
     // host-batch pipeline: three slots, one stream each (see *_host)
     struct Slot {
         hipStream_t s = nullptr;
@@ -235,31 +229,21 @@ size_t run_one(hyobfs_salamander* c, bool obf, const uint8_t* in, size_t in_len,
     return W;
 }
 
-// The context's scratch for stream s, grown to `need` bytes.  Caller holds c->ws_mu.
-void* stream_workspace(hyobfs_salamander* c, hipStream_t s, uint64_t need,
-                       hyobfs_salamander::StreamWs** entry = nullptr) {
-    hyobfs_salamander::StreamWs* e = nullptr;
-    for (auto& x : c->ws)
-        if (x.s == s) e = &x;
-    if (!e) {
-        c->ws.push_back(hyobfs_salamander::StreamWs{});
-        e = &c->ws.back();
-        e->s = s;
-    }
-    if (entry) *entry = e;
-    if (e->cap < need) {
-        if (e->p) {
-            // only launches on s use this buffer, and every one of them was
-            // enqueued under ws_mu: once s drains, nothing references it
-            if (hipStreamSynchronize(s) != hipSuccess) return nullptr;
-            (void)hipFree(e->p);
-        }
-        e->p = nullptr;
-        e->cap = 0;
-        if (hipMalloc(&e->p, need) != hipSuccess) return nullptr;
-        e->cap = need;
-    }
-    return e->p;
+// The context's scratch pool (created on first use).
+constexpr uint64_t kPoolKeepBytes = 32ull << 20;   // cached across calls; more is returned at sync points
+hipMemPool_t scratch_pool(hyobfs_salamander* c) {
+    std::lock_guard<std::mutex> lk(c->pool_mu);
+    if (c->pool) return c->pool;
+    hipMemPoolProps props{};
+    props.allocType = hipMemAllocationTypePinned;
+    props.location.type = hipMemLocationTypeDevice;
+    props.location.id = c->device;
+    hipMemPool_t p = nullptr;
+    if (hipMemPoolCreate(&p, &props) != hipSuccess) return nullptr;
+    uint64_t keep = kPoolKeepBytes;
+    (void)hipMemPoolSetAttribute(p, hipMemPoolAttrReleaseThreshold, &keep);
+    c->pool = p;
+    return p;
 }
 
 int validate_and_fill(hyobfs_salamander* c, const hyobfs_batch* b, bool obf, BatchParams& bp,
@@ -296,18 +280,6 @@ int validate_and_fill(hyobfs_salamander* c, const hyobfs_batch* b, bool obf, Bat
     return HYOBFS_OK;
 }
 
-// Bytes of the context's per-stream scratch a batch needs: the tile sums of a
-// packed batch without a caller workspace, then (the two-pass stream kernel)
-// 32 bytes of key per datagram.
-inline uint64_t ctx_ws_bytes(const hyobfs_salamander* c, const hyobfs_batch* b, uint64_t& keys_off) {
-    uint64_t need = 0;
-    if (b->n && b->out_stride == 0 && !b->workspace) need = (hyobfs_batch_workspace_size(b->n) + 255) & ~255ull;
-    keys_off = need;
-    const int kc = hyobfs::resolve_kernel(c->kernel);
-    if (b->n >= 2 && (kc == HYOBFS_KERNEL_STREAM || kc == HYOBFS_KERNEL_PIPE)) need += 32 * b->n;
-    return need;
-}
-
 int run_batch(hyobfs_salamander* c, const hyobfs_batch* b, void* stream, bool obf) {
     if (!c || !b) return HYOBFS_ERR_INVALID;
     DeviceGuard g(c->device);
@@ -316,55 +288,18 @@ int run_batch(hyobfs_salamander* c, const hyobfs_batch* b, void* stream, bool ob
     BatchParams bp;
     const int rc = validate_and_fill(c, b, obf, bp, s);
     if (rc != HYOBFS_OK) return rc;
-    std::unique_lock<std::mutex> ws_lk(c->ws_mu, std::defer_lock);
-    uint64_t keys_off = 0;
-    const hyobfs::SideLane* side = nullptr;
-    if (const uint64_t need = ctx_ws_bytes(c, b, keys_off)) {   // held through the launch (see StreamWs)
-        ws_lk.lock();
-        hyobfs_salamander::StreamWs* e = nullptr;
-        auto* w = static_cast<uint8_t*>(stream_workspace(c, s, need, &e));
-        if (!w) return HYOBFS_ERR_NOMEM;
-        if (keys_off) bp.tile_sums = reinterpret_cast<uint64_t*>(w);
-        if (need > keys_off) bp.keys = reinterpret_cast<uint64_t*>(w + keys_off);
-        if (bp.keys && hyobfs::resolve_kernel(c->kernel) == HYOBFS_KERNEL_PIPE) {
-            if (!e->side.s) {   // the side lane of this caller stream, kept until the context is freed
-                hyobfs::SideLane sl;
-                bool ok = hipStreamCreateWithFlags(&sl.s, hipStreamNonBlocking) == hipSuccess;
-                for (auto& ev : sl.ev)
-                    ok = ok && hipEventCreateWithFlags(&ev, hipEventDisableTiming) == hipSuccess;
-                if (!ok) {   // nothing half-made stays behind: the next call tries again
-                    for (auto& ev : sl.ev)
-                        if (ev) (void)hipEventDestroy(ev);
-                    if (sl.s) (void)hipStreamDestroy(sl.s);
-                    return HYOBFS_ERR_HIP;
-                }
-                e->side = sl;
-            }
-            side = &e->side;
-        }
+    void* scratch = nullptr;
+    if (b->n && b->out_stride == 0 && !b->workspace) {   // packed, no caller workspace: the context's pool
+        hipMemPool_t pool = scratch_pool(c);
+        if (!pool) return HYOBFS_ERR_HIP;
+        if (hipMallocFromPoolAsync(&scratch, hyobfs_batch_workspace_size(b->n), pool, s) != hipSuccess)
+            return HYOBFS_ERR_NOMEM;
+        bp.tile_sums = static_cast<uint64_t*>(scratch);
     }
-#ifdef HY_BOUNDS_CHECK
-    // debug variant: HYOBFS_DEBUG_IN_BYTES bounds the input; report the first bad access
-    static unsigned long long* dbg = nullptr;
-    if (!dbg && hipMalloc(reinterpret_cast<void**>(&dbg), 16 * sizeof(unsigned long long)) != hipSuccess)
-        return HYOBFS_ERR_NOMEM;
-    (void)hipMemsetAsync(dbg, 0, 16 * sizeof(unsigned long long), s);
-    bp.dbg = dbg;
-    const char* ib = std::getenv("HYOBFS_DEBUG_IN_BYTES");
-    bp.dbg_in_bytes = ib ? std::strtoull(ib, nullptr, 10) : ~0ull;
-    const int r2 = hyobfs::launch_salamander(obf, bp, c->kp, s, side) == hipSuccess ? HYOBFS_OK : HYOBFS_ERR_HIP;
-    unsigned long long h[16];
-    (void)hipStreamSynchronize(s);
-    (void)hipMemcpy(h, dbg, sizeof h, hipMemcpyDeviceToHost);
-    if (h[0])
-        std::fprintf(stderr, "HY_BOUNDS kind=%llu block=%llu thread=%llu v=%llu %llu %llu %llx n=%llu\n", h[0], h[1],
-                     h[2], h[3], h[4], h[5], h[6], (unsigned long long)bp.n);
-    return r2;
-#else
-    return hyobfs::launch_salamander(obf, bp, c->kp, s, side) == hipSuccess ? HYOBFS_OK : HYOBFS_ERR_HIP;
-#endif
+    const hipError_t e = hyobfs::launch_salamander(obf, bp, c->kp, s);
+    if (scratch && hipFreeAsync(scratch, s) != hipSuccess) return HYOBFS_ERR_HIP;   // after the launch, in stream order
+    return e == hipSuccess ? HYOBFS_OK : HYOBFS_ERR_HIP;
 }
-
 
 // One batch per shard, each on its own context's stream (and device): launch all, then wait for all.
 int run_sharded(hyobfs_salamander* const* ctxs, const hyobfs_batch* batches, int nshards, bool obf) {
@@ -539,13 +474,11 @@ void hyobfs_salamander_free(hyobfs_salamander* c) {
             (void)hipStreamSynchronize(c->stream);
             (void)hipStreamDestroy(c->stream);
         }
-        // the callers' streams may be gone by now: wait for the whole device
-        if (!c->ws.empty()) (void)hipDeviceSynchronize();
-        for (auto& e : c->ws) {
-            (void)hipFree(e.p);
-            for (auto& ev : e.side.ev)
-                if (ev) (void)hipEventDestroy(ev);
-            if (e.side.s) (void)hipStreamDestroy(e.side.s);
+        if (c->pool) {
+            // scratch frees are queued on the callers' streams, which may be gone
+            // by now: wait for the whole device before the pool goes
+            (void)hipDeviceSynchronize();
+            (void)hipMemPoolDestroy(c->pool);
         }
         if (c->stage) (void)hipHostFree(c->stage);
         for (auto& sl : c->slot) {
@@ -567,7 +500,7 @@ void hyobfs_salamander_free(hyobfs_salamander* c) {
 int hyobfs_salamander_device(const hyobfs_salamander* c) { return c ? c->device : -1; }
 
 int hyobfs_salamander_set_kernel(hyobfs_salamander* c, int kernel) {
-    if (!c || kernel < HYOBFS_KERNEL_AUTO || kernel > HYOBFS_KERNEL_FLAT) return HYOBFS_ERR_INVALID;
+    if (!c || kernel < HYOBFS_KERNEL_AUTO || kernel > HYOBFS_KERNEL_TILE) return HYOBFS_ERR_INVALID;
     c->kernel = kernel;
     return HYOBFS_OK;
 }

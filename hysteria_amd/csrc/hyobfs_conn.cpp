@@ -11,7 +11,9 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
 #include <mutex>
+#include <thread>
 #include <new>
 #include <vector>
 
@@ -58,7 +60,33 @@ struct hyobfs_conn {
     std::vector<iovec> riov, wiov;
     std::vector<sockaddr_storage> raddr;
     hyobfs::Coalescer* co = nullptr;       // set: per-datagram calls go through batches
+    std::atomic<bool> closing{false};      // Close() has begun: calls return -1, EBADF
+    std::atomic<int> inflight{0};          // threads inside read_from / write_to / *_batch
 };
+
+namespace {
+struct InFlight {   // a call in progress on the connection (close waits for it to leave)
+    hyobfs_conn* c;
+    explicit InFlight(hyobfs_conn* x) : c(x) { c->inflight.fetch_add(1, std::memory_order_acq_rel); }
+    ~InFlight() { c->inflight.fetch_sub(1, std::memory_order_acq_rel); }
+    bool closed() const {
+        if (!c->closing.load(std::memory_order_acquire)) return false;
+        errno = EBADF;
+        return true;
+    }
+};
+
+// Stops the coalescer (it sends what WriteTo accepted while the socket is still
+// open), then waits for every caller still inside the connection.
+void quiesce(hyobfs_conn* c, bool wake_readers) {
+    c->closing.store(true, std::memory_order_release);
+    hyobfs::coalescer_stop(c->co);
+    // a plain-mode ReadFrom blocked in recvfrom: shutdown wakes it (a 0-byte
+    // read, turned into EBADF below); Linux does this for unconnected UDP too
+    if (wake_readers) (void)shutdown(c->fd, SHUT_RD);
+    while (c->inflight.load(std::memory_order_acquire) > 0) std::this_thread::yield();
+}
+}  // namespace
 
 extern "C" {
 
@@ -84,18 +112,26 @@ int hyobfs_conn_wrap(int fd, hyobfs_salamander* ctx, uint32_t batch, hyobfs_conn
     return HYOBFS_OK;
 }
 
-void hyobfs_conn_free(hyobfs_conn* c) {
-    if (!c) return;
-    hyobfs::coalescer_free(c->co);   // sends what WriteTo accepted, stops its threads
+static void conn_release(hyobfs_conn* c) {
+    hyobfs::coalescer_free(c->co);   // (already stopped by quiesce)
     c->rx.release();
     c->tx.release();
     delete c;
 }
 
+void hyobfs_conn_free(hyobfs_conn* c) {
+    if (!c) return;
+    quiesce(c, false);   // sends what WriteTo accepted, stops the coalescer's threads
+    conn_release(c);
+}
+
 int hyobfs_conn_close(hyobfs_conn* c) {   // Close(), conn.go:101-103: closes the inner conn
     if (!c) return HYOBFS_ERR_INVALID;
+    // the coalescer flushes before the socket closes: every datagram WriteTo
+    // accepted is sent, and no thread of ours touches the fd number after close
+    quiesce(c, true);
     const int rc = close(c->fd);
-    hyobfs_conn_free(c);
+    conn_release(c);
     return rc == 0 ? HYOBFS_OK : HYOBFS_ERR_IO;
 }
 
@@ -105,12 +141,15 @@ int64_t hyobfs_conn_read_from(hyobfs_conn* c, uint8_t* p, size_t cap, void* addr
         errno = EINVAL;
         return -1;
     }
+    InFlight g(c);
+    if (g.closed()) return -1;
     if (c->co) return hyobfs::coalescer_read(c->co, p, cap, addr, addrlen);
     for (;;) {
         std::lock_guard<std::mutex> lk(c->read_mu);
         socklen_t al = addrlen ? *addrlen : 0;
         const ssize_t n = recvfrom(c->fd, c->read_buf, kBuf, 0, static_cast<sockaddr*>(addr), addr ? &al : nullptr);
         if (addrlen) *addrlen = al;
+        if (n <= 0 && g.closed()) return -1;   // woken by Close()
         if (n <= 0) return n;   // error or empty datagram: returned as is (:77-80)
         const size_t m = hyobfs_salamander_deobfuscate(c->ctx, c->read_buf, (size_t)n, p, cap);
         if (m > 0) return (int64_t)m;
@@ -124,6 +163,8 @@ int64_t hyobfs_conn_write_to(hyobfs_conn* c, const uint8_t* p, size_t len, const
         errno = EINVAL;
         return -1;
     }
+    InFlight g(c);
+    if (g.closed()) return -1;
     if (c->co) return hyobfs::coalescer_write(c->co, p, len, addr, addrlen);
     std::lock_guard<std::mutex> lk(c->write_mu);
     // Obfuscate into the 2048-byte writeBuf: 0 when len > 2040 (salamander.go:60-62)
@@ -139,6 +180,8 @@ int hyobfs_conn_read_batch(hyobfs_conn* c, hyobfs_dgram* msgs, uint32_t n) {
         return -1;
     }
     if (n == 0) return 0;
+    InFlight g(c);
+    if (g.closed()) return -1;
     if (c->co) {   // the coalescer's reader owns the socket's receive side
         errno = EBUSY;
         return -1;
@@ -156,6 +199,7 @@ int hyobfs_conn_read_batch(hyobfs_conn* c, hyobfs_dgram* msgs, uint32_t n) {
             c->rmsg[i].msg_hdr.msg_namelen = sizeof(sockaddr_storage);
         }
         const int k = recvmmsg(c->fd, c->rmsg.data(), n, MSG_WAITFORONE, nullptr);
+        if (k <= 0 && g.closed()) return -1;   // woken by Close()
         if (k <= 0) return k;
         for (int i = 0; i < k; ++i) c->rx.len[i] = c->rmsg[i].msg_len;
         hyobfs_batch b{};
@@ -194,6 +238,8 @@ int hyobfs_conn_write_batch(hyobfs_conn* c, const hyobfs_dgram* msgs, uint32_t n
         errno = EINVAL;
         return -1;
     }
+    InFlight g(c);
+    if (g.closed()) return -1;
     if (c->co) {
         errno = EBUSY;
         return -1;

@@ -28,10 +28,11 @@ __device__ __forceinline__ void hy_wave_sync() {
 }
 #endif
 
-constexpr int kTile = 256;          // datagrams per workgroup tile (= threads)
+constexpr int kTile = 256;          // datagrams per tile-sum entry of the packed layout's scan
 constexpr uint32_t kMaxDatagram = (1u << 24) - 64;  // longest datagram a batch accepts
-constexpr int HY_KERNEL_FLAT = 6;   // HYOBFS_KERNEL_FLAT: the wave kernel's boundary-free sweep
 constexpr uint64_t kMaxStride = 1ull << 24;         // longest slot of a slotted output
+// batch kernels (include/hyobfs.h HYOBFS_KERNEL_*)
+constexpr int kKernelAuto = 0, kKernelWave = 1, kKernelTile = 2;
 
 // BLAKE2b state for the per-packet key, precomputed on the host from the PSK
 // alone (salamander.go:88-91 hashes PSK || salt; every block before the one
@@ -58,38 +59,19 @@ struct BatchParams {
     uint8_t* out;
     uint64_t out_cap;
     uint64_t out_stride;    // 0 = packed
-    double inv_stride;      // 1.0 / out_stride (slotted chunk -> packet lookup)
     uint64_t* out_off;
     uint32_t* out_len;
     unsigned long long* out_total;
     const uint64_t* tile_prefix;  // packed: exclusive prefix of tile sums (ntiles+1)
     uint64_t* tile_sums;          // packed: scratch, ntiles+1 entries
-    uint64_t* keys;               // stream kernel: scratch, 4 key words per datagram (NULL: not available)
-    uint64_t part_len;            // main kernel: n / grid datagrams per workgroup ...
-    uint64_t part_rem;            // ... plus one for the first n % grid workgroups
     uint32_t run_log2;            // wave kernel: datagrams per run = 2^run_log2
-    uint32_t tile_stride;         // persistent kernel: 0 = one contiguous part per workgroup;
-                                  // G = workgroup g takes the 256-datagram tiles g, g+G, g+2G, ...
     int kernel;                   // HYOBFS_KERNEL_* of the context (0 = auto)
-    // HY_BOUNDS_CHECK builds only (build_variants/, never the shipped library):
-    // first out-of-range access recorded here instead of performed
-    unsigned long long* dbg;
-    uint64_t dbg_in_bytes;
 };
 
 // HYOBFS_KERNEL_* that a context's setting resolves to (AUTO: the
 // HYOBFS_KERNEL environment variable, else 0)
 int resolve_kernel(int ctx_kernel);
-// Side lane of the pipelined two-pass path (HYOBFS_KERNEL_PIPE): a second
-// stream on the caller's device for the key pass, and the events that order
-// each sweep chunk after its keys.  Owned by the context, one per caller stream.
-constexpr int kSideEvents = 64;
-struct SideLane {
-    hipStream_t s = nullptr;
-    hipEvent_t ev[kSideEvents] = {};
-};
-hipError_t launch_salamander(bool obfuscate, const BatchParams& b, const KeyParams& k,
-                             hipStream_t s, const SideLane* side = nullptr);
+hipError_t launch_salamander(bool obfuscate, const BatchParams& b, const KeyParams& k, hipStream_t s);
 hipError_t launch_keys(const KeyParams& k, const uint64_t* salts, uint8_t* keys, uint64_t n,
                        hipStream_t s);
 hipError_t launch_gecko_encode(const KeyParams& k, const hyobfs_gecko_batch& b, hipStream_t s);

@@ -1,45 +1,32 @@
-// salamander.hip -- gfx950 kernels for Hysteria's Salamander obfuscation.
+// salamander.hip -- gfx950 batch kernels for Hysteria's Salamander obfuscation:
+// launch dispatch, the packed layout's tile scan, the keys-only kernel and the
+// synthetic-input kernels.
 //
 // Reference semantics (apernet/hysteria): extras/obfs/salamander.go:59-91.
 //   Obfuscate:   out = salt(8) || in[i] ^ key[i % 32]        (:59-72)
 //   Deobfuscate: out[i] = in[8 + i] ^ key[i % 32], reject len <= 8  (:74-86)
 //   key = BLAKE2b-256(PSK || salt)                              (:88-91)
 //
-// Kernel shape ("Kernels"): a persistent grid of 256-thread
-// workgroups, each owning an equal contiguous range of datagrams, walked in
-// sub-tiles of 256 (lane t <-> datagram t).  Per sub-tile: lane t derives its
-// datagram's output width and offset (packed layout: wavefront scan), hashes
-// PSK||salt with BLAKE2b in registers -- one round at a time, interleaved with
-// the previous sub-tile's sweep -- and stores the key, pre-rotated to the
-// output's 32-byte phase, in LDS.  The sub-tile's output bytes are one
-// contiguous range; all 256 lanes sweep it in 16-byte chunks, 64 consecutive
-// chunks (1 KiB) per wave instruction.  A chunk inside one payload is one
-// unaligned 16-byte load, one LDS key read, four XORs and one aligned 16-byte
-// store; the few chunks at datagram edges are finished by their owning lane.
-// No MFMA: there is no contraction; the kernel is HBM-bound (2L+16 bytes per
-// obfuscated datagram).
-#include "salamander_stream.h"
+// Two batch kernels ("Kernels"), both HBM-bound byte work, no MFMA:
+//   * salamander_tile_kernel (salamander_tile.h): slotted batches whose region
+//     edges are all multiples of 8 -- the uniform 1200-byte headline batch.
+//     One-shot workgroups of 16 datagrams: a key wave beside three data waves.
+//   * salamander_wave_kernel (salamander_wave.h): every other layout (packed
+//     output, ragged lengths, any alignment).  One wave per 64-datagram group.
+#include "salamander_tile.h"
 
 namespace hyobfs {
 
-// The main kernel's instantiations live in salamander_inst.hip (one TU per salt word).
-#define HY_EXTERN_SW(n)                                                                              \
-    extern template void launch_main_sw<true, true, n>(const BatchParams&, const KeyParams&, hipStream_t);  \
-    extern template void launch_main_sw<true, false, n>(const BatchParams&, const KeyParams&, hipStream_t); \
-    extern template void launch_main_sw<false, true, n>(const BatchParams&, const KeyParams&, hipStream_t); \
-    extern template void launch_main_sw<false, false, n>(const BatchParams&, const KeyParams&, hipStream_t); \
+// The kernels' instantiations live in salamander_inst.hip (one TU per salt word).
+#define HY_EXTERN_SW(n)                                                                                   \
     extern template void launch_wave_sw<true, true, n>(const BatchParams&, const KeyParams&, hipStream_t);  \
     extern template void launch_wave_sw<true, false, n>(const BatchParams&, const KeyParams&, hipStream_t); \
     extern template void launch_wave_sw<false, true, n>(const BatchParams&, const KeyParams&, hipStream_t); \
     extern template void launch_wave_sw<false, false, n>(const BatchParams&, const KeyParams&, hipStream_t); \
-    extern template void launch_uniform_sw<true, n>(const BatchParams&, const KeyParams&, const UniformParams&,    \
-                                                    hipStream_t);                                                  \
-    extern template void launch_uniform_sw<false, n>(const BatchParams&, const KeyParams&, const UniformParams&,   \
-                                                     hipStream_t);                                                  \
-    extern template void launch_stream_sw<true, n>(const BatchParams&, const KeyParams&, const StreamParams&,      \
-                                                   uint64_t, uint64_t, hipStream_t, const SideLane*);               \
-    extern template void launch_stream_sw<false, n>(const BatchParams&, const KeyParams&, const StreamParams&,     \
-                                                    uint64_t, uint64_t, hipStream_t, const SideLane*);
+    extern template void launch_tile_sw<true, n>(const BatchParams&, const KeyParams&, const TileParams&,   \
+                                                 hipStream_t);                                              \
+    extern template void launch_tile_sw<false, n>(const BatchParams&, const KeyParams&, const TileParams&,  \
+                                                  hipStream_t);
 HY_EXTERN_SW(0) HY_EXTERN_SW(1) HY_EXTERN_SW(2) HY_EXTERN_SW(3) HY_EXTERN_SW(4) HY_EXTERN_SW(5)
 HY_EXTERN_SW(6) HY_EXTERN_SW(7) HY_EXTERN_SW(8) HY_EXTERN_SW(9) HY_EXTERN_SW(10) HY_EXTERN_SW(11)
 HY_EXTERN_SW(12) HY_EXTERN_SW(13) HY_EXTERN_SW(14) HY_EXTERN_SW(15)
@@ -158,45 +145,40 @@ __global__ void synth_bimodal_kernel(uint32_t* dst, uint64_t n, uint64_t seed, u
 
 // ------------------------------------------------------------------ launchers
 
-// Kernel choice ("Kernels"): every batch runs the wave-group kernel
-// (salamander_wave.h) unless the persistent workgroup kernel
-// (salamander_device.h) is asked for.  HYOBFS_KERNEL=wave|persistent|... forces one.
+// Kernel choice ("Kernels"): AUTO runs the tile kernel where it
+// applies (tile_params) and the wave kernel elsewhere; WAVE forces the wave
+// kernel; TILE asks for the tile kernel (falls back to the wave kernel where it
+// does not apply).  HYOBFS_KERNEL=wave|tile sets what AUTO means in a process.
 static int kernel_override() {   // HYOBFS_KERNEL, as HYOBFS_KERNEL_* (0 = auto)
     static int v = -1;
     if (v == -1) {
         const char* e = std::getenv("HYOBFS_KERNEL");
-        v = !e ? 0
-               : std::strcmp(e, "wave") == 0         ? 1
-               : std::strcmp(e, "persistent") == 0   ? 2
-               : std::strcmp(e, "uniform") == 0      ? 3
-               : std::strcmp(e, "stream") == 0       ? 4
-               : std::strcmp(e, "pipe") == 0         ? 5
-               : std::strcmp(e, "flat") == 0         ? 6
-                                                      : 0;
+        v = !e ? kKernelAuto : std::strcmp(e, "wave") == 0 ? kKernelWave : std::strcmp(e, "tile") == 0 ? kKernelTile
+                                                                                                     : kKernelAuto;
     }
     return v;
 }
-
-static int kernel_choice(const BatchParams& bp) { return bp.kernel ? bp.kernel : kernel_override(); }
 
 int resolve_kernel(int ctx_kernel) { return ctx_kernel ? ctx_kernel : kernel_override(); }
 
 template <bool OBF, bool PACKED>
 static void launch_main(const BatchParams& bp, const KeyParams& k, hipStream_t s) {
-    const int kc = kernel_choice(bp);
-    // auto: the wave-group kernel for both layouts (round 2: with 128 park slots per
-    // group it beats the persistent kernel on the bimodal mix)
-    const bool wave = kc != 2;
-    BatchParams b = bp;
-    b.kernel = kc;   // resolved (context or HYOBFS_KERNEL): the wave launcher picks its sweep from it
+    const int kc = resolve_kernel(bp.kernel);
+    TileParams T;
+    if (!PACKED && kc != kKernelWave && tile_params<OBF>(bp, T)) {
+        switch (k.salt_pos >> 3) {
+#define HY_CASE(n) \
+    case n: launch_tile_sw<OBF, n>(bp, k, T, s); break;
+            HY_CASE(0) HY_CASE(1) HY_CASE(2) HY_CASE(3) HY_CASE(4) HY_CASE(5) HY_CASE(6) HY_CASE(7)
+            HY_CASE(8) HY_CASE(9) HY_CASE(10) HY_CASE(11) HY_CASE(12) HY_CASE(13) HY_CASE(14)
+            HY_CASE(15)
+#undef HY_CASE
+        }
+        return;
+    }
     switch (k.salt_pos >> 3) {
-#define HY_CASE(n)                                   \
-    case n:                                          \
-        if (wave)                                    \
-            launch_wave_sw<OBF, PACKED, n>(b, k, s); \
-        else                                         \
-            launch_main_sw<OBF, PACKED, n>(b, k, s); \
-        break;
+#define HY_CASE(n) \
+    case n: launch_wave_sw<OBF, PACKED, n>(bp, k, s); break;
         HY_CASE(0) HY_CASE(1) HY_CASE(2) HY_CASE(3) HY_CASE(4) HY_CASE(5) HY_CASE(6) HY_CASE(7)
         HY_CASE(8) HY_CASE(9) HY_CASE(10) HY_CASE(11) HY_CASE(12) HY_CASE(13) HY_CASE(14)
         HY_CASE(15)
@@ -204,69 +186,11 @@ static void launch_main(const BatchParams& bp, const KeyParams& k, hipStream_t s
     }
 }
 
-// Uniform batches (salamander_uniform.h): the runs of two datagrams on the
-// uniform kernel; an odd last datagram through the wave kernel (its metadata
-// is reported by the uniform launch).
-template <bool OBF>
-static bool try_uniform(const BatchParams& b, const KeyParams& k, hipStream_t s, const SideLane* side) {
-    // only when asked for: on 1M x 1200 B both measure slower than the wave
-    // kernel (uniform 0.56 vs 0.50 ms, two-pass 0.47-0.62 vs 0.46)
-    const int kc = kernel_choice(b);
-    if (kc < 3 || kc > 5) return false;
-    UniformParams P;
-    StreamParams SP;
-    uint32_t W = 0;
-    // two passes: keys, then one-shot sweep (pipe: keys on the side lane)
-    if (kc >= 4 && stream_params<OBF>(b, SP)) {
-        const SideLane* sl = kc == 5 ? side : nullptr;
-        W = SP.W;
-        switch (k.salt_pos >> 3) {
-#define HY_CASE(sw) \
-    case sw: launch_stream_sw<OBF, sw>(b, k, SP, b.n / 2, b.n, s, sl); break;
-            HY_CASE(0) HY_CASE(1) HY_CASE(2) HY_CASE(3) HY_CASE(4) HY_CASE(5) HY_CASE(6) HY_CASE(7)
-            HY_CASE(8) HY_CASE(9) HY_CASE(10) HY_CASE(11) HY_CASE(12) HY_CASE(13) HY_CASE(14)
-            HY_CASE(15)
-#undef HY_CASE
-        }
-    } else if (uniform_params<OBF>(b, P)) {
-        W = P.W;
-        switch (k.salt_pos >> 3) {
-#define HY_CASE(n) \
-    case n: launch_uniform_sw<OBF, n>(b, k, P, s); break;
-            HY_CASE(0) HY_CASE(1) HY_CASE(2) HY_CASE(3) HY_CASE(4) HY_CASE(5) HY_CASE(6) HY_CASE(7)
-            HY_CASE(8) HY_CASE(9) HY_CASE(10) HY_CASE(11) HY_CASE(12) HY_CASE(13) HY_CASE(14)
-            HY_CASE(15)
-#undef HY_CASE
-        }
-    } else {
-        return false;
-    }
-    if (b.n & 1) {   // the odd last datagram; its metadata came with the launch above
-        const uint64_t last = b.n - 1;
-        BatchParams t = b;
-        t.n = 1;
-        t.in = b.in + last * b.in_stride;
-        if (OBF) t.salts = b.salts + last;
-        t.out = b.out + last * W;   // 16-aligned: last is even and W a multiple of 8
-        t.out_cap = W;
-        t.out_stride = W;
-        t.inv_stride = 1.0 / (double)W;
-        t.out_off = nullptr;
-        t.out_len = nullptr;
-        t.out_total = nullptr;
-        t.kernel = 1;
-        launch_main<OBF, false>(t, k, s);
-    }
-    return true;
-}
-
-hipError_t launch_salamander(bool obf, const BatchParams& b, const KeyParams& k, hipStream_t s,
-                             const SideLane* side) {
+hipError_t launch_salamander(bool obf, const BatchParams& b, const KeyParams& k, hipStream_t s) {
     if (b.n == 0) return hipSuccess;
     const uint64_t ntiles = div_up(b.n, kTile);
     if (ntiles > 0x7fffffffull) return hipErrorInvalidValue;
     if (k.nblk == 2 && (k.salt_pos >> 3) != 15) return hipErrorInvalidValue;   // by construction
-    if (obf ? try_uniform<true>(b, k, s, side) : try_uniform<false>(b, k, s, side)) return hipGetLastError();
     BatchParams bp = b;
     if (b.out_stride == 0) {
         const dim3 grid((uint32_t)ntiles), block(kTile);
@@ -281,7 +205,6 @@ hipError_t launch_salamander(bool obf, const BatchParams& b, const KeyParams& k,
         else
             launch_main<false, true>(bp, k, s);
     } else {
-        bp.inv_stride = 1.0 / (double)b.out_stride;
         if (obf)
             launch_main<true, false>(bp, k, s);
         else

@@ -1,24 +1,16 @@
-// salamander_inst.hip -- instantiates the main kernel for one salt word
+// salamander_inst.hip -- instantiates the batch kernels for one salt word
 // (compiled once per HY_SW = 0..15, see Makefile).
-#include "salamander_stream.h"
+#include "salamander_tile.h"
 
 #ifndef HY_SW
 #error "compile with -DHY_SW=<salt word 0..15>"
 #endif
 
 namespace hyobfs {
-template void launch_main_sw<true, true, HY_SW>(const BatchParams&, const KeyParams&, hipStream_t);
-template void launch_main_sw<true, false, HY_SW>(const BatchParams&, const KeyParams&, hipStream_t);
-template void launch_main_sw<false, true, HY_SW>(const BatchParams&, const KeyParams&, hipStream_t);
-template void launch_main_sw<false, false, HY_SW>(const BatchParams&, const KeyParams&, hipStream_t);
 template void launch_wave_sw<true, true, HY_SW>(const BatchParams&, const KeyParams&, hipStream_t);
 template void launch_wave_sw<true, false, HY_SW>(const BatchParams&, const KeyParams&, hipStream_t);
 template void launch_wave_sw<false, true, HY_SW>(const BatchParams&, const KeyParams&, hipStream_t);
 template void launch_wave_sw<false, false, HY_SW>(const BatchParams&, const KeyParams&, hipStream_t);
-template void launch_uniform_sw<true, HY_SW>(const BatchParams&, const KeyParams&, const UniformParams&, hipStream_t);
-template void launch_uniform_sw<false, HY_SW>(const BatchParams&, const KeyParams&, const UniformParams&, hipStream_t);
-template void launch_stream_sw<true, HY_SW>(const BatchParams&, const KeyParams&, const StreamParams&, uint64_t,
-                                            uint64_t, hipStream_t, const SideLane*);
-template void launch_stream_sw<false, HY_SW>(const BatchParams&, const KeyParams&, const StreamParams&, uint64_t,
-                                             uint64_t, hipStream_t, const SideLane*);
+template void launch_tile_sw<true, HY_SW>(const BatchParams&, const KeyParams&, const TileParams&, hipStream_t);
+template void launch_tile_sw<false, HY_SW>(const BatchParams&, const KeyParams&, const TileParams&, hipStream_t);
 }  // namespace hyobfs

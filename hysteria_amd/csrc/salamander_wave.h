@@ -35,17 +35,8 @@ constexpr int kWavesPerBlock = 4;    // independent waves per workgroup
 #define HY_WU 8
 #endif
 constexpr int kWU = HY_WU;           // chunks per lane per sweep iteration
-#ifndef HY_FLAT_U
-#define HY_FLAT_U 8                  // the boundary-free sweep: chunks per lane per iteration
-#endif
-#ifndef HY_FLAT_MIN_WAVES
-#define HY_FLAT_MIN_WAVES 8          // ... and its waves per SIMD
-#endif
 #ifndef HY_RUN_LOG2
 #define HY_RUN_LOG2 3
-#endif
-#ifndef HY_PREFETCH
-#define HY_PREFETCH 0                // 1: software-pipelined sweep (two register sets)
 #endif
 #ifndef HY_WAVE_MIN_WAVES
 #define HY_WAVE_MIN_WAVES 8          // __launch_bounds__ min waves per SIMD
@@ -176,11 +167,7 @@ __device__ __forceinline__ void group_contrib(const GroupBuf& G, const uint8_t* 
         u128 X = 0;
         if (PL >= 16) {   // one 16-byte window inside the payload, shifted into place
             const int ws = min(max(base, 0), (int)PL - 16);
-#ifdef HY_X_NOBLOAD   // ablation builds only (timing experiments; wrong output)
-            const u128 V = (u128)(uintptr_t)(src + ws);
-#else
             const u128 V = load16u(src + ws);
-#endif
             const int d = ws - base;
             X = d >= 0 ? (V << (8 * d)) : (V >> (8 * -d));
         } else {
@@ -262,10 +249,8 @@ __device__ __forceinline__ uint32_t park_index(uint2 ow, uint32_t c) {
     return c == cs ? 0u : (c == cs + 1 && cs + 1 <= ce) ? 1u : (c == ce && ce > cs + 1) ? 2u : 3u;
 }
 
-// FLAT = the boundary-free sweep (flat_sweep below) for slotted batches whose
-// datagrams all have regions of 16 bytes or more and none is dropped.
-template <bool OBF, bool PACKED, int SW, bool FLAT = false>
-__global__ __launch_bounds__(kGroup* kWavesPerBlock, FLAT ? HY_FLAT_MIN_WAVES : HY_WAVE_MIN_WAVES) void
+template <bool OBF, bool PACKED, int SW>
+__global__ __launch_bounds__(kGroup* kWavesPerBlock, HY_WAVE_MIN_WAVES) void
 salamander_wave_kernel(BatchParams B, KeyParams K) {
     constexpr uint32_t SALT = OBF ? 8u : 0u;   // salt bytes in front of the output payload
     constexpr uint32_t SKIP = OBF ? 0u : 8u;   // salt bytes in front of the input payload
@@ -282,13 +267,7 @@ salamander_wave_kernel(BatchParams B, KeyParams K) {
     // on neighbouring runs and the chip sweeps memory in address order.
     const uint32_t rl = B.run_log2, RUN = 1u << rl;
     const uint64_t Wt = (uint64_t)gridDim.x * kWavesPerBlock;
-#ifdef HY_XCD_REMAP   // A/B builds only: consecutive logical blocks on one XCD (bijective remap)
-    const uint32_t nwg = gridDim.x, ob = blockIdx.x, xq = nwg / 8, xr = nwg % 8, xcd = ob % 8;
-    const uint32_t lb = (xcd < xr ? xcd * (xq + 1) : xr * (xq + 1) + (xcd - xr) * xq) + ob / 8;
-    const uint64_t w = (uint64_t)lb * kWavesPerBlock + wid;
-#else
     const uint64_t w = (uint64_t)blockIdx.x * kWavesPerBlock + wid;
-#endif
     const uint32_t j = (uint32_t)lane >> rl, i = (uint32_t)lane & (RUN - 1);
     const uint64_t r = (uint64_t)j * Wt + w;   // this lane's run
     const uint64_t p = (r << rl) + i;          // this lane's datagram
@@ -391,78 +370,6 @@ salamander_wave_kernel(BatchParams B, KeyParams K) {
     }
     hy_wave_sync();
 
-    if constexpr (FLAT) {
-        // ---- 3'. boundary-free sweep (uniform slotted batches whose lengths, slots and
-        // input offsets are multiples of 8).  Every region edge then falls on an 8-byte
-        // boundary, so each 8-byte half of a 16-byte chunk is exactly one of: a salt,
-        // 8 payload bytes of one datagram, or nothing.  The chunk's datagrams are q (the
-        // last region starting at or before it) and q + 1.  Each half is one 8-byte
-        // load (or the salt) XOR the key qword, all in the sweep's own loads: no early
-        // boundary windows, no parking, and every lane runs the same instructions.
-        // Only halves that belong to another run are left out (byte-masked store).
-        const uint32_t nchunks = (totm + 15u) >> 4;
-        constexpr int UF = HY_FLAT_U;
-        constexpr uint32_t STEP = kGroup * UF;
-        // half x of the chunk at a: class (0 none, 1 salt, 2 payload), datagram, input address
-        auto half_src = [&](uint32_t qq, uint32_t x, uint32_t& k, uint64_t& addr) -> uint32_t {
-            const uint2 owq = G.ow[qq];
-            const uint2 own = qq + 1 < cnt ? G.ow[qq + 1] : make_uint2(0u, 0u);
-            if (owq.y && x >= owq.x && x < owq.x + owq.y) {   // (x < owq.x: the chunks before the first run)
-                k = qq;
-            } else if (own.y && x >= own.x && x < own.x + own.y) {
-                k = qq + 1;
-            } else {
-                return 0u;
-            }
-            const uint32_t ox = G.ow[k].x;
-            if (OBF && x == ox) return 1u;
-            addr = G.io[k] + (x - ox - SALT);
-            return 2u;
-        };
-        for (uint32_t c0 = 0; c0 < nchunks; c0 += STEP) {
-            uint64_t v0[UF], v1[UF];
-            uint32_t cls[UF];   // per half: class (2 bits) | datagram (6 bits) << 2
-#pragma unroll
-            for (int u = 0; u < UF; ++u) {   // every load first
-                const uint32_t c = c0 + u * kGroup + lane, a = c << 4;
-                v0[u] = 0;
-                v1[u] = 0;
-                cls[u] = 0;
-                if (c < nchunks) {
-                    const uint32_t qq = group_search(G, a);
-                    uint32_t k0 = 0, k1 = 0;
-                    uint64_t a0 = 0, a1 = 0;
-                    const uint32_t c0s = half_src(qq, a, k0, a0), c1s = half_src(qq, a + 8, k1, a1);
-                    if (c0s == 2u && c1s == 2u && k0 == k1) {   // inside one payload: one 16-byte load
-                        const u128 x = load16_nt(in + a0);
-                        v0[u] = (uint64_t)x;
-                        v1[u] = (uint64_t)(x >> 64);
-                    } else {
-                        if (c0s == 2u) v0[u] = load8_nt(in + a0);
-                        if (c1s == 2u) v1[u] = load8_nt(in + a1);
-                    }
-                    cls[u] = c0s | k0 << 2 | c1s << 8 | k1 << 10;
-                }
-            }
-#pragma unroll
-            for (int u = 0; u < UF; ++u) {
-                const uint32_t c = c0 + u * kGroup + lane, a = c << 4, h = (a >> 4) & 1u;
-                const uint32_t c0s = cls[u] & 3u, k0 = (cls[u] >> 2) & 63u;
-                const uint32_t c1s = (cls[u] >> 8) & 3u, k1 = (cls[u] >> 10) & 63u;
-                if (!c0s && !c1s) continue;
-                const uint4 kk0 = G.key[2 * k0 + h], kk1 = G.key[2 * k1 + h];
-                const uint64_t lo = c0s == 2u ? v0[u] ^ ((uint64_t)kk0.y << 32 | kk0.x) : OBF ? G.salt[k0] : 0ull;
-                const uint64_t hi = c1s == 2u ? v1[u] ^ ((uint64_t)kk1.w << 32 | kk1.z) : OBF ? G.salt[k1] : 0ull;
-                uint8_t* dst = B.out + G.delta[c0s ? k0 : k1] + a;
-                if (c0s && c1s)
-                    store16_stream(dst, (u128)hi << 64 | lo);
-                else
-                    store_masked(dst, (u128)hi << 64 | lo, c0s ? 0x00FFu : 0xFF00u);
-            }
-        }
-        return;
-    }
-
     // ---- 3. boundary chunks datagram `lane` owns (the first datagram touching a
     // chunk owns it: exclusive max-scan of region ends) that are not inside one
     // payload.  A complete one that the sweep's lookup (park_owner/park_index)
@@ -536,7 +443,6 @@ salamander_wave_kernel(BatchParams B, KeyParams K) {
             if (R.fast[u]) {
                 R.v[u] = load16_nt(in + G.io[qq] + (a - owq.x - SALT));
             }
-#ifndef HY_X_NOPARK
             else if (c < nchunks) {   // parked boundary chunk?
                 uint2 owo;
                 const uint32_t o = park_owner(G, a, qq, owq, owo);
@@ -550,7 +456,6 @@ salamander_wave_kernel(BatchParams B, KeyParams K) {
                     }
                 }
             }
-#endif
         }
     };
     auto retire = [&](uint32_t c0, const Sweep& R) {
@@ -565,24 +470,11 @@ salamander_wave_kernel(BatchParams B, KeyParams K) {
         }
     };
     constexpr uint32_t STEP = kGroup * U;
-#if HY_PREFETCH
-    // two register sets: iteration i+1's loads are in flight while i retires
-    Sweep RA, RB;
-    if (nchunks) issue(0, RA);
-    for (uint32_t c0 = 0; c0 < nchunks; c0 += 2 * STEP) {
-        const bool h1 = c0 + STEP < nchunks, h2 = c0 + 2 * STEP < nchunks;
-        if (h1) issue(c0 + STEP, RB);
-        retire(c0, RA);
-        if (h2) issue(c0 + 2 * STEP, RA);
-        if (h1) retire(c0 + STEP, RB);
-    }
-#else
     for (uint32_t c0 = 0; c0 < nchunks; c0 += STEP) {
         Sweep R;
         issue(c0, R);
         retire(c0, R);
     }
-#endif
 
     // ---- 5. late boundary chunks (not parked): byte-masked stores.  The salt
     // slots now hold parked chunks, so salts come from the batch.
@@ -635,35 +527,12 @@ inline uint32_t wave_run_log2() {
     return (uint32_t)v;
 }
 
-// The boundary-free sweep applies when every datagram of a slotted batch has the
-// same length (a multiple of 8, like the slot stride and the input stride), a
-// region of 16 bytes or more, and nothing is dropped: then a 16-byte chunk touches
-// at most two regions and splits between them at its middle if at all.
-template <bool OBF>
-inline bool flat_ok(const BatchParams& b) {
-    if (b.out_stride == 0 || b.in_len || b.in_off || b.n == 0) return false;
-    const uint64_t L = b.len_uniform;
-    if (L > kMaxDatagram || L < (OBF ? 16u : 24u)) return false;
-    // every region edge and input qword on an 8-byte boundary
-    if ((L | b.out_stride | b.in_stride | reinterpret_cast<uintptr_t>(b.in)) & 7u) return false;
-    const uint64_t W = OBF ? L + 8 : L - 8;
-    if ((b.pkt_cap && W > b.pkt_cap) || W > b.out_stride) return false;
-    return (b.n - 1) * b.out_stride + W <= b.out_cap;
-}
-
 template <bool OBF, bool PACKED, int SW>
 void launch_wave_sw(const BatchParams& bp, const KeyParams& k, hipStream_t s) {
     const uint64_t ngroups = div_up(bp.n, kGroup);
     const uint64_t blocks = div_up(ngroups, kWavesPerBlock);
     BatchParams b = bp;
     b.run_log2 = PACKED ? wave_packed_run_log2() : wave_run_log2();
-    if constexpr (!PACKED) {
-        if (b.kernel == HY_KERNEL_FLAT && flat_ok<OBF>(b)) {
-            hipLaunchKernelGGL((salamander_wave_kernel<OBF, false, SW, true>), dim3((uint32_t)blocks),
-                               dim3(kGroup * kWavesPerBlock), 0, s, b, k);
-            return;
-        }
-    }
     hipLaunchKernelGGL((salamander_wave_kernel<OBF, PACKED, SW>), dim3((uint32_t)blocks),
                        dim3(kGroup * kWavesPerBlock), 0, s, b, k);
 }

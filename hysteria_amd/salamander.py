@@ -136,11 +136,11 @@ class SalamanderObfuscator:
     def __exit__(self, *exc):
         self.close()
 
-    KERNELS = {"auto": 0, "wave": 1, "persistent": 2, "uniform": 3, "stream": 4, "pipe": 5, "flat": 6}
+    KERNELS = {"auto": 0, "wave": 1, "tile": 2}
 
     def set_kernel(self, kernel: str) -> None:
-        """Batch kernel of this context: "auto" (the wave-group kernel), "wave", "persistent", "uniform",
-        "stream", "pipe" or "flat" (include/hyobfs.h, HYOBFS_KERNEL_*)."""
+        """Batch kernel of this context: "auto" (the tile kernel where it applies, else the
+        wave-group kernel), "wave" (forced) or "tile" (include/hyobfs.h, HYOBFS_KERNEL_*)."""
         check(self._lib.hyobfs_salamander_set_kernel(self._h, self.KERNELS[kernel]), "set_kernel")
 
     # ------------------------------------------------------------ salt source

@@ -90,32 +90,19 @@ void hyobfs_salamander_free(hyobfs_salamander* ctx);
 int hyobfs_salamander_device(const hyobfs_salamander* ctx);
 
 /* Batch kernel of this context (no reference counterpart: a tuning knob).
-   HYOBFS_KERNEL_AUTO picks the wave-group kernel for slotted and packed
-   batches (HYOBFS_KERNEL_PERSISTENT forces the persistent workgroup kernel,
-   the packed default until round 2).  For uniform batches (equal lengths, a
-   multiple of 8, payloads of 512 B or more, dense 16-aligned input and
-   output, nothing dropped) two more kernels can be asked for:
-   HYOBFS_KERNEL_UNIFORM (aligned-load sweep over runs of two datagrams) and
-   HYOBFS_KERNEL_STREAM (keys pass into context scratch pipelined with one-shot
-   4 KiB sweeps); both measure slower than AUTO on 1M x 1200 B.
-   HYOBFS_KERNEL_PIPE is STREAM with the keys pass on a second stream the
-   context owns (one per caller stream), each sweep chunk ordered after its keys
-   by an event, so the key grid never holds a sweep launch open.
-   HYOBFS_KERNEL_FLAT is the wave kernel with a boundary-free sweep (each chunk
-   composed from at most two datagrams in the sweep itself) for slotted batches
-   of one length (16 B or more; 24 B or more to deobfuscate) with nothing dropped.
-   The HYOBFS_KERNEL environment variable (wave|persistent|uniform|stream|pipe|flat)
-   overrides AUTO.  UNIFORM, STREAM, PIPE or FLAT on a batch that does not qualify falls back
-   to the AUTO choice.  Returns HYOBFS_ERR_INVALID for an unknown value.
+   HYOBFS_KERNEL_AUTO runs the tile kernel on slotted batches whose region edges
+   are all multiples of 8 (one length, slot and input stride multiples of 8,
+   payloads of 16 bytes or more, nothing dropped, no 16-byte chunk holding two
+   datagrams' payload bytes) -- the uniform 1200-byte batch of the benchmark --
+   and the wave-group kernel on every other batch (packed output, ragged
+   lengths, any alignment).  HYOBFS_KERNEL_WAVE forces the wave-group kernel;
+   HYOBFS_KERNEL_TILE is AUTO.  The HYOBFS_KERNEL environment variable
+   (wave|tile) overrides AUTO.  Returns HYOBFS_ERR_INVALID for an unknown value.
    Outputs are identical. */
 enum {
     HYOBFS_KERNEL_AUTO = 0,
     HYOBFS_KERNEL_WAVE = 1,
-    HYOBFS_KERNEL_PERSISTENT = 2,
-    HYOBFS_KERNEL_UNIFORM = 3,
-    HYOBFS_KERNEL_STREAM = 4,
-    HYOBFS_KERNEL_PIPE = 5,
-    HYOBFS_KERNEL_FLAT = 6
+    HYOBFS_KERNEL_TILE = 2
 };
 int hyobfs_salamander_set_kernel(hyobfs_salamander* ctx, int kernel);
 
@@ -170,10 +157,11 @@ size_t hyobfs_salamander_deobfuscate(hyobfs_salamander* ctx, const uint8_t* in,
  *
  * `out` must be 16-byte aligned.  All pointers are device-accessible; the
  * call only enqueues work on `stream` (a hipStream_t; NULL = the HIP null
- * stream, as everywhere in HIP) and returns.  workspace: device scratch of at least
- * hyobfs_batch_workspace_size(n) bytes, or NULL to use a context-owned buffer
- * (then the first call of a new maximum size allocates and is not
- * graph-capturable).
+ * stream, as everywhere in HIP) and returns.  workspace (packed layout only):
+ * device scratch of at least hyobfs_batch_workspace_size(n) bytes, or NULL:
+ * then the scratch is allocated stream-ordered from a context-owned memory pool
+ * and freed behind the launch on the same stream (any number of caller streams
+ * and threads; the pool keeps at most 32 MiB cached between calls).
  */
 typedef struct hyobfs_batch {
     uint64_t n;

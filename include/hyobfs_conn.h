@@ -53,9 +53,15 @@ typedef struct hyobfs_dgram {
 /* Wrap a bound UDP socket.  The connection does not own ctx.  batch = the
    largest number of datagrams per batched call (0 = 1024). */
 int hyobfs_conn_wrap(int fd, hyobfs_salamander* ctx, uint32_t batch, hyobfs_conn** out);
-/* Close(): closes the socket and frees the connection. */
+/* Close(): sends what a coalescing connection accepted, wakes every thread
+   blocked in a call on the connection (they return -1 with errno EBADF, as a
+   Go ReadFrom returns once Close closes the inner conn), waits for them to
+   leave, closes the socket and frees the connection.  Calls that START after
+   close began are invalid (the handle is gone). */
 int hyobfs_conn_close(hyobfs_conn* c);
-/* frees the connection, leaves the socket open */
+/* Frees the connection, leaves the socket open.  Coalescing callers are woken
+   as by close; in plain mode no call may be in progress (nothing wakes a
+   recvfrom on a socket that stays open). */
 void hyobfs_conn_free(hyobfs_conn* c);
 
 /* ReadFrom: bytes written to p (>= 0), or -1 with errno set (socket error). */
@@ -80,8 +86,14 @@ int hyobfs_conn_write_batch(hyobfs_conn* c, const hyobfs_dgram* msgs, uint32_t n
        thread seals the batch when it holds max_batch datagrams or max_wait_us
        after its first one, obfuscates it as one GPU batch and sends it with
        sendmmsg while the next batch fills.  Like a UDP sendto, a datagram is
-       accepted once queued; a later send failure is counted in the stats, not
-       returned.  Writers block while both batches are busy (backpressure).
+       accepted once queued.  DIVERGENCE from conn.go:93-98 (which returns the
+       socket error to the WriteTo whose datagram failed): a send that fails
+       after its write_to returned is counted in the stats and its errno is
+       returned by the NEXT write_to on the connection (-1, that call's
+       datagram not accepted), once.  Salts come from the context's RandSrc
+       (hyobfs_salamander_seed / _next_salts), not from a caller-supplied
+       source; the wire format is unchanged.  Writers block while both
+       batches are busy (backpressure).
      - hyobfs_conn_read_from is served from batches a reader thread receives
        with recvmmsg and deobfuscates as one GPU batch: invalid datagrams are
        dropped and an empty datagram is a 0-byte read, as ReadFrom does; the
@@ -90,7 +102,7 @@ int hyobfs_conn_write_batch(hyobfs_conn* c, const hyobfs_dgram* msgs, uint32_t n
        return -1 with errno EBUSY.
    Latency added per datagram: up to max_wait_us plus one GPU batch.  Call once,
    before the connection is used; hyobfs_conn_free / _close send what was
-   accepted, then stop the threads. */
+   accepted (before _close closes the socket), then stop the threads. */
 int hyobfs_conn_set_coalescing(hyobfs_conn* c, uint32_t max_batch, uint32_t max_wait_us);
 /* Blocks until every datagram write_to accepted so far was handed to the socket. */
 int hyobfs_conn_flush(hyobfs_conn* c);

@@ -267,3 +267,82 @@ def run_coalesce_scenarios(device: int = 0, writers: int = 8, per_writer: int = 
         raw.close()
         oa.close()
         ob.close()
+
+
+def run_lifecycle_scenarios(device: int = 0, n: int = 200, max_batch: int = 64, max_wait_us: int = 100000):
+    """Close() and error paths of both modes (include/hyobfs_conn.h):
+      * close() without flush() on a coalescing connection still sends every
+        datagram write_to accepted (the flusher runs before the socket closes);
+      * close() while other threads are blocked in read_from / write_to wakes
+        them with EBADF (coalescing and plain mode; conn.go:101-103 Close of the
+        inner conn unblocks a pending ReadFrom);
+      * a send that fails after write_to queued its datagram (coalescing) is
+        reported by the NEXT write_to as -1 with that errno, then cleared.
+    A long max_wait_us keeps the datagrams queued until close() or flush()."""
+    import threading
+    import time
+    rng = np.random.default_rng(23)
+    oa = SalamanderObfuscator(PSK, device)
+    raw = _udp()
+    raw.setsockopt(socket.SOL_SOCKET, socket.SO_RCVBUF, 8 << 20)
+    r_addr = raw.getsockname()
+    try:
+        # 1. accepted but not flushed: close() sends them
+        ca = SalamanderPacketConn(_udp(), oa, batch=max_batch)
+        ca.set_coalescing(max_batch, max_wait_us)
+        a_addr = ca.local_addr()
+        sent = [_payload(rng, 1 + (i * 37) % 1300) for i in range(n)]
+        for p in sent:
+            assert ca.write_to(p, r_addr) == len(p)
+        ca.close()
+        got = []
+        raw.settimeout(10.0)
+        for _ in sent:
+            wire, addr = raw.recvfrom(4096)
+            assert addr == a_addr
+            got.append(ref.deobfuscate(PSK, wire))
+        assert sorted(got) == sorted(sent)
+
+        # 2. close() wakes blocked readers (and a writer blocked on a full queue)
+        for coalescing in (True, False):
+            cb = SalamanderPacketConn(_udp(), oa, batch=max_batch)
+            if coalescing:
+                cb.set_coalescing(max_batch, max_wait_us)
+            errs = []
+
+            def blocked_read():
+                try:
+                    cb.read_from()
+                    errs.append("returned")
+                except OSError as e:
+                    errs.append(e.errno)
+            ts = [threading.Thread(target=blocked_read) for _ in range(3 if coalescing else 1)]
+            for t in ts:
+                t.start()
+            time.sleep(0.3)
+            cb.close()
+            for t in ts:
+                t.join(20)
+                assert not t.is_alive(), "reader still blocked after close()"
+            assert errs == [errno.EBADF] * len(ts), (coalescing, errs)
+
+        # 3. a failed send after write_to returned: reported by the next write_to.
+        # A limited broadcast without SO_BROADCAST fails in sendmmsg with EACCES.
+        cc = SalamanderPacketConn(_udp(), oa, batch=max_batch)
+        cc.set_coalescing(max_batch, 50)
+        assert cc.write_to(b"to nowhere", ("255.255.255.255", r_addr[1])) == 10
+        cc.flush()
+        assert cc.stats()["tx_errors"] == 1
+        try:
+            cc.write_to(b"next", r_addr)
+            raise AssertionError("send error not reported")
+        except OSError as e:
+            assert e.errno == errno.EACCES, e
+        assert cc.write_to(b"after", r_addr) == 5   # reported once, then cleared
+        cc.flush()
+        wire, _ = raw.recvfrom(4096)
+        assert ref.deobfuscate(PSK, wire) == b"after"
+        cc.close()
+    finally:
+        raw.close()
+        oa.close()

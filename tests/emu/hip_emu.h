@@ -157,6 +157,13 @@ inline unsigned long long __ballot(int pred) {
 // convert it to unsigned first, exactly as on the GPU)
 inline int hyemu_readfirstlane(int v) { return hyemu::xchg(v, 0); }
 #define __builtin_amdgcn_readfirstlane(x) hyemu_readfirstlane((int)(x))
+// DPP quad_perm only (dpp_ctrl 0x00-0xFF): lane i of each quad reads lane ctrl[i]
+inline int hyemu_mov_dpp(int v, int ctrl) {
+    if (ctrl < 0 || ctrl > 0xFF) std::abort();
+    const int lane = (int)(threadIdx.x & 63);
+    return hyemu::xchg(v, (lane & ~3) | ((ctrl >> (2 * (lane & 3))) & 3));
+}
+#define __builtin_amdgcn_mov_dpp(v, ctrl, rm, bm, bc) hyemu_mov_dpp((int)(v), (ctrl))
 inline uint32_t hyemu_alignbit(uint32_t hi, uint32_t lo, uint32_t s) {
     return (uint32_t)((((uint64_t)hi << 32) | lo) >> (s & 31));
 }
@@ -217,3 +224,22 @@ inline hipError_t hipHostMalloc(void** p, size_t n, unsigned) { return hipMalloc
 inline hipError_t hipHostFree(void* p) { return hipFree(p); }
 inline hipError_t hipHostGetDevicePointer(void** d, void* h, unsigned) { *d = h; return hipSuccess; }
 inline hipError_t hipMemsetAsync(void* p, int v, size_t n, hipStream_t) { std::memset(p, v, n); return hipSuccess; }
+// stream-ordered pool allocation (launches run synchronously here)
+typedef void* hipMemPool_t;
+enum hipMemAllocationType { hipMemAllocationTypePinned = 1 };
+enum hipMemLocationType { hipMemLocationTypeDevice = 1 };
+enum hipMemPoolAttr { hipMemPoolAttrReleaseThreshold = 4 };
+struct hipMemLocation {
+    hipMemLocationType type;
+    int id;
+};
+struct hipMemPoolProps {
+    hipMemAllocationType allocType;
+    int handleTypes;
+    hipMemLocation location;
+};
+inline hipError_t hipMemPoolCreate(hipMemPool_t* p, const hipMemPoolProps*) { *p = (hipMemPool_t)1; return hipSuccess; }
+inline hipError_t hipMemPoolSetAttribute(hipMemPool_t, hipMemPoolAttr, void*) { return hipSuccess; }
+inline hipError_t hipMemPoolDestroy(hipMemPool_t) { return hipSuccess; }
+inline hipError_t hipMallocFromPoolAsync(void** p, size_t n, hipMemPool_t, hipStream_t) { return hipMalloc(p, n); }
+inline hipError_t hipFreeAsync(void* p, hipStream_t) { return hipFree(p); }

@@ -89,6 +89,17 @@ def case_uniform(n, L, obf):
             len_uniform=L + 8)
 
 
+def case_slotted(n, L, obf, slot_pad, in_pad, psk_len):
+    """Uniform lengths into slots of W + slot_pad bytes (gap bytes must stay
+    untouched), inputs at a stride of L + in_pad, a PSK of psk_len bytes."""
+    psk = bytes((7 * i + 1) & 0xFF for i in range(psk_len))
+    W = L + 8 if obf else L - 8
+    stride, istride = W + slot_pad, L + in_pad
+    inp = np.frombuffer(ref.stream_bytes(1, 0, n * istride + 16), np.uint8).copy()
+    salts = ref.splitmix64_array(2, 0, n)
+    run(obf, psk, None, None, inp, salts, n * stride, out_stride=stride, in_stride=istride, len_uniform=L)
+
+
 def case_slotted_far(n, L, stride_mb, obf):
     """Slotted output whose slots sit beyond 2^31: the output buffer is an untouched
     anonymous mapping, so only the written slots cost memory."""
@@ -267,6 +278,8 @@ if __name__ == "__main__":
     args = [int(a) for a in sys.argv[2:]]
     if which == "bimodal":
         case_bimodal(args[0], bool(args[1]))
+    elif which == "slotted":
+        case_slotted(args[0], args[1], bool(args[2]), args[3], args[4], args[5])
     elif which == "uniform":
         case_uniform(args[0], args[1], bool(args[2]))
     elif which == "host":
@@ -280,6 +293,10 @@ if __name__ == "__main__":
         from conn_cases import run_coalesce_scenarios
         run_coalesce_scenarios(writers=args[0], per_writer=args[1], readers=args[2], max_batch=args[3],
                                idle_timeout=30.0)   # emulated batches run slowly under a loaded CPU tier
+    elif which == "lifecycle":
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        from conn_cases import run_lifecycle_scenarios
+        run_lifecycle_scenarios(n=args[0], max_batch=args[1])
     elif which == "far":
         case_slotted_far(args[0], args[1], args[2], bool(args[3]))
     elif which == "ragged":

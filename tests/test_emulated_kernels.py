@@ -1,8 +1,8 @@
 """CPU tier: the HIP kernel sources, compiled for the host against tests/emu/hip_emu.h
 (CPU emulation of the HIP subset they use) under AddressSanitizer, checked
 against the C oracle.  This exercises the kernels' indexing, the packed-layout
-scan, chunk ownership, sub-tile pipelining and the partition logic without a
-GPU, and fails on any out-of-bounds access.  Test infrastructure only: the
+scan, chunk ownership, the tile kernel's chunk classes and quad hash, and the
+host paths without a GPU, and fails on any out-of-bounds access.  Test infrastructure only: the
 product library (hysteria_amd/libhyobfs.so) is never built this way."""
 import glob
 import os
@@ -34,25 +34,15 @@ def emu_lib():
 
 # Each test's case: (run_case.py arguments, extra environment), from its parameters.
 SPECS = {
-    "test_emulated_uniform_kernel": lambda p: (p["which"], p["args"], {"HYOBFS_KERNEL": "uniform", "HYEMU_CUS": "2"}),
-    "test_emulated_stream_kernel": lambda p: (p["which"], p["args"], {"HYOBFS_KERNEL": "stream", "HYEMU_CUS": "2"}),
-    "test_emulated_stream_kernel_pipelined": lambda p: (
-        "uniform", p["args"], {"HYOBFS_KERNEL": "stream", "HYEMU_CUS": "2", "HYOBFS_STREAM_FIRST_RUNS": "12",
-                               "HYOBFS_STREAM_GROW": "2"}),
-    "test_emulated_flat_sweep": lambda p: (p["which"], p["args"], {"HYOBFS_KERNEL": "flat", "HYEMU_CUS": "2"}),
-    "test_emulated_pipe_kernel": lambda p: (
-        "uniform", p["args"], {"HYOBFS_KERNEL": "pipe", "HYEMU_CUS": "2", "HYOBFS_PIPE_FIRST_RUNS": "12",
-                               "HYOBFS_PIPE_GROW": "2", "HYOBFS_PIPE_KEY_BLOCKS": "1"}),
+    "test_emulated_tile_kernel": lambda p: (p["which"], p["args"], {"HYOBFS_KERNEL": "tile", "HYEMU_CUS": "2"}),
+    "test_emulated_wave_kernel_forced": lambda p: None if p["which"] in ("conn", "host", "coalesce", "quic",
+                                                                         "lifecycle") else (
+        p["which"], p["args"], {"HYEMU_CUS": p["cus"], "HYOBFS_KERNEL": "wave"}),
     "test_emulated_wave_kernel_run_lengths": lambda p: (
         p["which"], p["args"], {"HYOBFS_RUN_LOG2": p["run_log2"], "HYOBFS_KERNEL": "wave"}),
     "test_emulated_wave_kernel_packed_run_lengths": lambda p: (
         p["which"], p["args"], {"HYOBFS_PACKED_RUN_LOG2": p["run_log2"], "HYOBFS_RUN_LOG2": p["run_log2"],
                                 "HYOBFS_KERNEL": "wave"}),
-    "test_emulated_persistent_kernel": lambda p: None if p["which"] in ("conn", "host", "coalesce", "quic") else (
-        p["which"], p["args"], {"HYEMU_CUS": p["cus"], "HYOBFS_KERNEL": "persistent"}),
-    "test_emulated_persistent_kernel_strided": lambda p: (
-        p["which"], p["args"], {"HYEMU_CUS": p["cus"], "HYOBFS_KERNEL": "persistent",
-                                "HYOBFS_PERSIST_ORDER": "strided"}),
     "test_emulated_kernel_vs_oracle": lambda p: (p["which"], p["args"], {"HYEMU_CUS": p["cus"]}),
 }
 
@@ -111,6 +101,7 @@ CASES = [
     ("host", "1000 300 96 0", "2"),
     ("conn", "64 120", "2"),             # UDP loopback through the conn wrapper (conn.go)
     ("coalesce", "8 150 4 32", "2"),     # many threads on one coalescing conn (hyobfs_conn_set_coalescing)
+    ("lifecycle", "60 16", "2"),         # close() flushes, wakes blocked callers; deferred send errors
     ("far", "200 300 15 1", "8"),        # workgroup bases beyond 2^31
     ("far", "200 300 15 0", "8"),
     ("gecko", "40 7", "2"),              # Gecko frame encode + parse kernels (gecko.hip), aligned sweep
@@ -136,68 +127,26 @@ RUN_CASES = [
 ]
 
 
-# The uniform kernel (salamander_uniform.h): equal lengths, multiples of 8, dense
-# slots, payloads of 512 B and more; odd counts (the last datagram through the
-# wave kernel), odd word counts (1192), the shortest eligible runs (512 B
-# payloads: 65 chunks per run), several blocks (3000), and lengths that are not
-# eligible (1201, 504, 8, 16: the wave kernel).
-UNIFORM_CASES = [
-    ("uniform", "257 1200 1"), ("uniform", "256 1200 0"), ("uniform", "301 1192 1"),
-    ("uniform", "301 1192 0"), ("uniform", "300 512 1"), ("uniform", "300 512 0"),
-    ("uniform", "129 1400 1"), ("uniform", "3001 1200 0"), ("uniform", "3000 1200 1"),
-    ("uniform", "99 1201 1"), ("uniform", "99 504 1"), ("uniform", "129 8 0"), ("uniform", "64 16 1"),
-]
+# The tile kernel (salamander_tile.h): slotted batches whose region edges are all
+# multiples of 8.  Dense slots of 8 mod 16 (obfuscate 1200 -> 1208) and 0 mod 16,
+# gapped slots (gap bytes untouched), input strides with padding, partial last
+# tiles, large slots (fewer datagrams per tile), every salt-word position of the
+# PSK (lengths 4..127, including the two-block case 121..127), and layouts that
+# do not qualify (odd lengths, deobfuscate into dense slots of 8 mod 16: the wave kernel).
+TILE_CASES = [
+    ("uniform", "257 1200 1"), ("uniform", "256 1200 0"), ("uniform", "301 1192 1"), ("uniform", "301 1192 0"),
+    ("uniform", "33 16 1"), ("uniform", "33 24 0"), ("uniform", "300 17 1"), ("uniform", "99 1201 0"),
+    ("slotted", "70 1200 1 24 8 16"), ("slotted", "70 1208 0 8 0 16"), ("slotted", "45 2040 1 0 16 9"),
+    ("slotted", "37 4096 0 16 0 31"), ("slotted", "21 9000 1 0 0 16"), ("slotted", "40 64 1 0 0 4"),
+    ("slotted", "40 64 0 0 24 5"), ("slotted", "23 100 1 4 4 16"),
+] + [("slotted", f"18 {L} 1 {pad} 0 {k}") for k, L, pad in
+     [(4, 40, 0), (8, 48, 8), (12, 136, 0), (20, 200, 16), (60, 96, 0), (100, 1000, 8), (119, 512, 0),
+      (120, 256, 0), (121, 256, 8), (124, 512, 0), (127, 264, 0), (128, 64, 0), (300, 1200, 0)]]
 
 
-@pytest.mark.parametrize("which,args", UNIFORM_CASES)
-def test_emulated_uniform_kernel(emu_lib, which, args):
-    _run(emu_lib, which, args, {"HYOBFS_KERNEL": "uniform", "HYEMU_CUS": "2"})
-
-
-# the stream kernel's cases: the uniform ones without the 3000-datagram batches
-# (the pipelined test below covers many chunks at smaller sizes)
-STREAM_CASES = [c for c in UNIFORM_CASES if int(c[1].split()[0]) < 1000]
-
-
-@pytest.mark.parametrize("which,args", STREAM_CASES)
-def test_emulated_stream_kernel(emu_lib, which, args):
-    """The two-pass path (salamander_stream.h): keys into the context's scratch, then
-    one-shot waves over contiguous chunk regions (same cases as the uniform kernel)."""
-    _run(emu_lib, which, args, {"HYOBFS_KERNEL": "stream", "HYEMU_CUS": "2"})
-
-
-@pytest.mark.parametrize("args", ["1001 1200 0", "1000 1200 1", "999 1192 1", "600 512 0"])
-def test_emulated_stream_kernel_pipelined(emu_lib, args):
-    """Many chunks (first chunk 12 runs, doubling): every launch sweeps one chunk and
-    keys the next; region carries across chunk ends."""
-    _run(emu_lib, "uniform", args, {"HYOBFS_KERNEL": "stream", "HYEMU_CUS": "2",
-                                    "HYOBFS_STREAM_FIRST_RUNS": "12", "HYOBFS_STREAM_GROW": "2"})
-
-
-
-
-# the wave kernel's boundary-free sweep (HYOBFS_KERNEL=flat): uniform slotted batches at
-# every chunk phase (lengths 16..24 and odd ones), run edges, the 2048-byte maximum,
-# and layouts that do not qualify (fall back to the parked sweep)
-FLAT_CASES = [c for c in UNIFORM_CASES if int(c[1].split()[0]) < 1000] + [
-    ("uniform", "300 16 1"), ("uniform", "300 17 1"), ("uniform", "300 23 1"), ("uniform", "300 24 0"),
-    ("uniform", "300 25 0"), ("uniform", "257 1203 1"), ("uniform", "257 1209 0"), ("uniform", "130 2040 1"),
-    ("uniform", "130 2048 0"), ("uniform", "300 16 0"), ("far", "200 296 15 1"), ("far", "200 296 15 0"),
-    ("ragged", "9 1500 2100 1 1"), ("ragged", "12 700 100 1 0"),
-]
-
-
-@pytest.mark.parametrize("which,args", FLAT_CASES)
-def test_emulated_flat_sweep(emu_lib, which, args):
-    _run(emu_lib, which, args, {"HYOBFS_KERNEL": "flat", "HYEMU_CUS": "2"})
-
-
-@pytest.mark.parametrize("args", ["1001 1200 0", "1000 1200 1", "999 1192 1", "64 16 1"])
-def test_emulated_pipe_kernel(emu_lib, args):
-    """HYOBFS_KERNEL_PIPE: keys of every chunk on the side lane (chunk 0 by a full
-    grid, later chunks grid-striding over one workgroup), sweeps on the caller's stream."""
-    _run(emu_lib, "uniform", args, {"HYOBFS_KERNEL": "pipe", "HYEMU_CUS": "2", "HYOBFS_PIPE_FIRST_RUNS": "12",
-                                    "HYOBFS_PIPE_GROW": "2", "HYOBFS_PIPE_KEY_BLOCKS": "1"})
+@pytest.mark.parametrize("which,args", TILE_CASES)
+def test_emulated_tile_kernel(emu_lib, which, args):
+    _run(emu_lib, which, args, {"HYOBFS_KERNEL": "tile", "HYEMU_CUS": "2"})
 
 
 @pytest.mark.parametrize("which,args,run_log2", RUN_CASES)
@@ -213,23 +162,12 @@ def test_emulated_wave_kernel_packed_run_lengths(emu_lib, which, args, run_log2)
                                 "HYOBFS_KERNEL": "wave"})
 
 
-# the persistent kernel with interleaved tiles (workgroup g: tiles g, g+G, ...)
-STRIDED_CASES = [c for c in CASES if c[0] in ("uniform", "bimodal", "ragged", "far")]
-
-
-@pytest.mark.parametrize("which,args,cus", STRIDED_CASES)
-def test_emulated_persistent_kernel_strided(emu_lib, which, args, cus):
-    """HYOBFS_PERSIST_ORDER=strided: each packed tile's offset from the tile prefix,
-    tiles of one workgroup G apart (edge chunks shared between workgroups)."""
-    _run(emu_lib, which, args, {"HYEMU_CUS": cus, "HYOBFS_KERNEL": "persistent", "HYOBFS_PERSIST_ORDER": "strided"})
-
-
 @pytest.mark.parametrize("which,args,cus", CASES)
-def test_emulated_persistent_kernel(emu_lib, which, args, cus):
-    """The persistent workgroup kernel (HYOBFS_KERNEL=persistent) on the same cases."""
-    if which in ("conn", "host", "coalesce", "quic"):
+def test_emulated_wave_kernel_forced(emu_lib, which, args, cus):
+    """The wave-group kernel (HYOBFS_KERNEL=wave) on every case, also where AUTO runs the tile kernel."""
+    if which in ("conn", "host", "coalesce", "quic", "lifecycle"):
         pytest.skip("kernel-independent host paths run once, under the default kernel")
-    _run(emu_lib, which, args, {"HYEMU_CUS": cus, "HYOBFS_KERNEL": "persistent"})
+    _run(emu_lib, which, args, {"HYEMU_CUS": cus, "HYOBFS_KERNEL": "wave"})
 
 
 @pytest.mark.parametrize("which,args,cus", CASES)

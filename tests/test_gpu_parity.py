@@ -17,13 +17,12 @@ pytestmark = pytest.mark.gpu
 PSK = b"average_password"
 
 
-@pytest.fixture(scope="module", params=["auto", "wave", "persistent", "uniform", "stream", "pipe", "flat"])
+@pytest.fixture(scope="module", params=["auto", "wave", "tile"])
 def obfs(gpu, request):
-    """One context per batch kernel: auto (the shipped per-layout choice), and
-    each kernel forced on every layout (salamander_wave.h, salamander_device.h;
-    the uniform and two-pass stream kernels, salamander_uniform.h and
-    salamander_stream.h, apply to uniform batches and fall back to the auto
-    choice elsewhere)."""
+    """One context per batch kernel choice: auto (the shipped per-layout choice:
+    the tile kernel where it applies, salamander_tile.h, else the wave kernel),
+    the wave-group kernel forced on every layout (salamander_wave.h), and tile
+    (= auto, kept as the explicit name)."""
     import hysteria_amd
     o = hysteria_amd.SalamanderObfuscator(PSK, 0)
     o.set_kernel(request.param)
@@ -535,6 +534,15 @@ def test_packet_conn_loopback(gpu):
 
 
 @pytest.mark.gpu
+def test_packet_conn_lifecycle(gpu):
+    """close() without flush sends what write_to accepted; close() wakes blocked
+    readers with EBADF; a failed queued send is reported by the next write_to."""
+    import sys, os
+    sys.path.insert(0, os.path.dirname(__file__))
+    from conn_cases import run_lifecycle_scenarios
+    run_lifecycle_scenarios(device=0)
+
+
 def test_packet_conn_coalescing_loopback(gpu):
     """Coalescing mode: 8 writer and 4 reader threads on the per-datagram calls of one
     connection each side, GPU batches behind them; wire bytes against the oracle."""
