@@ -70,13 +70,10 @@ def parse():
 
 
 def kernel_src_sha() -> str:
-    """sha256 over the kernel sources: keys the committed PMC traffic figures."""
-    h = hashlib.sha256()
-    for p in sorted(glob.glob(os.path.join(ROOT, "hysteria_amd", "csrc", "*"))):
-        if os.path.isfile(p) and p.endswith((".h", ".hip", ".cpp", "Makefile")):
-            h.update(os.path.basename(p).encode())
-            h.update(open(p, "rb").read())
-    return h.hexdigest()[:16]
+    """sha256 over the kernel sources: keys the committed PMC traffic figures (scripts/src_sha.py)."""
+    sys.path.insert(0, os.path.join(ROOT, "scripts"))
+    from src_sha import src_sha
+    return src_sha()
 
 
 def pmc_traffic(workload: str, direction: str, datagrams: int, length) -> dict | None:
@@ -86,6 +83,9 @@ def pmc_traffic(workload: str, direction: str, datagrams: int, length) -> dict |
     except (OSError, ValueError, AttributeError):
         return None
     sha = kernel_src_sha()
+    import hysteria_amd
+    if hysteria_amd.build_id() != sha:   # the loaded library was not built from these sources
+        return None
     for e in entries:
         if (e.get("src_sha") == sha and e.get("workload") == workload and e.get("direction") == direction
                 and e.get("datagrams") == datagrams and e.get("len") == length):
@@ -301,7 +301,7 @@ def main():
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None, "kernel": KERNEL_NAMES[workload][args.kernel],
                 "algorithmic_bytes_per_launch": w["obf_bytes"], "avg_launch_ms": round(ev_obf * 1e3, 4),
-                "kernel_src_sha": kernel_src_sha()}
+                "kernel_src_sha": kernel_src_sha(), "lib_build_id": hy.build_id()}
         t = pmc_traffic(workload, "obfuscate", w["n"], w["len"])
         if t:
             roof["traffic"] = t["hbm_bytes_per_launch"]

@@ -13,6 +13,7 @@ from .salamander import (  # noqa: F401
     UDP_BUFFER_SIZE,
     PSKTooShortError,
     SalamanderObfuscator,
+    build_id,
     deobfuscate_batch_sharded,
     device_count,
     new_salamander_obfuscator,
@@ -28,5 +29,5 @@ __all__ = [
     "SalamanderObfuscator", "device_count", "new_salamander_obfuscator", "synth_bimodal_lengths",
     "synth_stream", "synth_u64", "workspace_size", "SalamanderPacketConn", "wrap_packet_conn_salamander",
     "obfuscate_batch_sharded", "deobfuscate_batch_sharded", "gecko", "GeckoOptions", "GeckoPacketConn",
-    "wrap_packet_conn_gecko",
+    "wrap_packet_conn_gecko", "build_id",
 ]

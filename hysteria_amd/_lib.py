@@ -72,13 +72,18 @@ def header_functions(path: str = HEADER_PATH) -> list[str]:
 
 
 _lib = None
+_variants = {}   # other builds loaded side by side (in-process A/B runs, scripts/ab_variants.py)
 
 
 def load(path: str = LIB_PATH) -> ctypes.CDLL:
-    """Load libhyobfs.so and declare the ABI.  Raises OSError if it is missing."""
+    """Load libhyobfs.so and declare the ABI.  Raises OSError if it is missing.
+    A different ``path`` loads that build beside the default one (each CDLL keeps
+    its own symbols)."""
     global _lib
-    if _lib is not None:
+    if path == LIB_PATH and _lib is not None:
         return _lib
+    if path != LIB_PATH and path in _variants:
+        return _variants[path]
     if not os.path.exists(path):
         raise OSError(f"{path} is missing: build it with `make -C hysteria_amd/csrc` "
                       "(or __graft_entry__.build()); there is no CPU fallback")
@@ -87,6 +92,7 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
     pctx = ctypes.c_void_p
     sig = {
         "hyobfs_abi_version": (i32, []),
+        "hyobfs_build_id": (ctypes.c_char_p, []),
         "hyobfs_status_string": (ctypes.c_char_p, [i32]),
         "hyobfs_device_count": (i32, []),
         "hyobfs_salamander_new": (i32, [vp, sz, i32, ctypes.POINTER(ctypes.c_void_p)]),
@@ -128,7 +134,10 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         f = getattr(lib, name)
         f.restype = res
         f.argtypes = args
-    _lib = lib
+    if path == LIB_PATH:
+        _lib = lib
+    else:
+        _variants[path] = lib
     return lib
 
 

@@ -425,6 +425,14 @@ extern "C" {
 
 int hyobfs_abi_version(void) { return HYOBFS_ABI_VERSION; }
 
+#if __has_include("build_id.h")
+#include "build_id.h"   // generated by the Makefile: the kernel-source hash
+#endif
+#ifndef HYOBFS_BUILD_ID
+#define HYOBFS_BUILD_ID "unknown"
+#endif
+const char* hyobfs_build_id(void) { return HYOBFS_BUILD_ID; }
+
 const char* hyobfs_status_string(int st) {
     switch (st) {
         case HYOBFS_OK: return "ok";

@@ -5,21 +5,21 @@
 //
 // A workgroup of four waves owns a TILE of 16 consecutive datagrams and exits
 // when it is done.  16 slots of a multiple of 8 bytes are whole 128-byte lines,
-// so no line is shared by two workgroups (which may sit on different XCDs).
-//   * wave 0 (keys): loads the 16 salts and hashes BLAKE2b-256(PSK || salt)
-//     with four lanes per key (one G column each, the diagonal step by DPP
-//     quad permutes), about 1k VALU instructions for all 16 keys, into LDS.
-//   * waves 1-3 (data): each thread classifies its kTU output chunks (16 bytes,
-//     1 KiB per wave instruction) and issues their loads at once.  With every
-//     region edge on an 8-byte boundary, each 8-byte half of a chunk is a salt,
-//     8 payload bytes of one datagram, or nothing, and one 16-byte window inside
-//     a payload holds every payload half of the chunk.  After one LDS-only
-//     barrier (the loads stay in flight across it, so they overlap the hash),
-//     each payload half is XORed with its key word and the chunk is stored.
-// The access shape is the one-shot region copy of a few KiB per wave, the
-// fastest copy shape measured on MI355X (tools/region_copy.hip).  Slots larger
-// than 16 x 192 x kTU / 16 bytes take several passes.  Applies when
-// tile_params() holds; everything else runs the wave kernel.
+// so no output line is shared by two workgroups (which may sit on different XCDs).
+//   1. waves 1-3 copy the tile's input range (16 x in_stride bytes at most) into
+//      LDS with LDS-DMA (global_load_lds_dwordx4, non-temporal): 1 KiB per
+//      instruction, 16-byte aligned and contiguous -- the loads of a plain
+//      copy, with nothing held in registers.
+//   2. meanwhile wave 0 loads the 16 salts and hashes BLAKE2b-256(PSK || salt)
+//      with four lanes per key (one G column each, the diagonal step by DPP
+//      quad permutes): about 1k VALU instructions for all 16 keys, into LDS.
+//   3. after one barrier, all four waves compose the output: with every region
+//      edge on an 8-byte boundary each 8-byte half of a 16-byte output chunk is
+//      a salt, 8 payload bytes of one datagram (one 8-byte LDS read XOR one key
+//      word) or nothing; one 16-byte non-temporal store per chunk, 1 KiB per
+//      wave instruction, whole lines.
+// Slots larger than 256 x kTSU x 16 / 16 bytes take several passes of step 3.
+// Applies when tile_params() holds; everything else runs the wave kernel.
 #pragma once
 #include "salamander_wave.h"
 
@@ -27,11 +27,6 @@ namespace hyobfs {
 
 constexpr int kTileMaxD = 16;        // datagrams per tile: one wave hashes 16 keys, 4 lanes each;
                                      // 16 slots of a multiple of 8 bytes are whole 128-byte lines
-#ifndef HY_TILE_U
-#define HY_TILE_U 7
-#endif
-constexpr int kTU = HY_TILE_U;       // output chunks per data thread and pass (192 x 7 x 16 B = 21 KiB:
-                                     // one pass for 16 slots of up to 1344 bytes)
 constexpr uint64_t kMaxTileSlot = 1u << 20;
 #ifndef HY_TILE_MIN_WAVES
 #define HY_TILE_MIN_WAVES 8
@@ -40,8 +35,18 @@ constexpr uint64_t kMaxTileSlot = 1u << 20;
 struct TileParams {
     uint32_t S;      // output slot (out_stride), a multiple of 8
     uint32_t W;      // output width, a multiple of 8, 16 <= W <= S
+    uint32_t LI;     // input bytes per datagram (len_uniform)
     float invS;      // 1 / S
 };
+
+#ifndef HY_TILE_SU
+#define HY_TILE_SU 5             // staged: output chunks per thread and pass (256 x 5 x 16 B = 20 KiB)
+#endif
+constexpr int kTSU = HY_TILE_SU;
+#ifndef HY_TILE_DMA_AUX
+#define HY_TILE_DMA_AUX 2        // cache policy of the staging loads: 2 = nt (streamed once; 4 % faster
+                                 // than the default policy, profiles/r03_ab_tile_stage.txt)
+#endif
 
 // BLAKE2b sigma, for compile-time placement of message words on the lanes
 struct B2Sigma {
@@ -233,99 +238,28 @@ __device__ __forceinline__ void store16_global(uint8_t* p, uint64_t lo, uint64_t
 #endif
 }
 
-// Per-chunk record kept across the barrier (one register):
-//   bits 0-7  key word index of the low half in s_key (datagram * 8 + word; the
-//             high half's word follows it, keys are stored twice in a row)
-//   bits 8-11 datagram whose salt the chunk carries
-//   bit 12/13 low/high half written; bit 14/15 low/high half is a salt
-//   bit 16    low half from the window's high 8 bytes; bit 17 high half from its low 8
-constexpr uint32_t kTcVlo = 1u << 12, kTcVhi = 1u << 13, kTcSlo = 1u << 14, kTcShi = 1u << 15;
-constexpr uint32_t kTcLoFromHi = 1u << 16, kTcHiFromLo = 1u << 17;
-
-// One output chunk: classification (tc record) and its 16-byte input window.
-template <bool OBF>
-__device__ __forceinline__ uint32_t tile_chunk(const uint8_t* __restrict__ ib, uint32_t in_stride, uint32_t S,
-                                               uint32_t W, float invS, uint32_t nt, uint32_t tbytes, uint32_t x,
-                                               u128& v) {
-    constexpr uint32_t SALT = OBF ? 8u : 0u;   // salt bytes in front of the output payload
-    constexpr uint32_t SKIP = OBF ? 0u : 8u;   // salt bytes in front of the input payload
-    v = 0;
-    if (x >= tbytes) return 0;
-    uint32_t p = (uint32_t)((float)x * invS);   // datagram of the low half (float estimate, fixed below)
-    int32_t r = (int32_t)(x - p * S);
-    if (r < 0) {
-        --p;
-        r += (int32_t)S;
-    } else if (r >= (int32_t)S) {
-        ++p;
-        r -= (int32_t)S;
-    }
-    uint32_t r2 = (uint32_t)r + 8u, p2 = p;   // the high half
-    if (r2 >= S) {
-        r2 -= S;
-        ++p2;
-    }
-    const bool vlo = (uint32_t)r < W;   // (then p < nt: x < tbytes)
-    const bool vhi = p2 < nt && r2 < W;
-    const bool slo = OBF && (uint32_t)r < 8u, shi = OBF && r2 < 8u;
-    const bool plo = vlo && !slo, phi = vhi && !shi;
-    const uint32_t jlo = (uint32_t)r - SALT, jhi = r2 - SALT;   // payload offsets (when payload)
-    uint32_t f = (vlo ? kTcVlo : 0u) | (vhi ? kTcVhi : 0u) | (slo ? kTcSlo : 0u) | (shi ? kTcShi : 0u);
-    f |= ((slo ? p : p2) & 15u) << 8;   // (p2 may be nt when no half is a salt)
-    uint32_t wp = p, wj = jlo;          // window: datagram, payload offset
-    if (plo) {
-        // tile_params: a payload half next to another datagram's payload half never occurs
-        if (!(phi && p2 == p)) {   // the payload's last word: the window ends with it
-            wj = jlo - 8u;
-            f |= kTcLoFromHi;
-        }
-        f |= p * 8u + ((jlo >> 3) & 3u);
-    } else if (phi) {
-        wp = p2;
-        wj = jhi;
-        f |= kTcHiFromLo | (p2 * 8u + ((jhi >> 3) & 3u) + 3u);
-    }
-#ifdef HY_X_TILE_ALIGN   // ablation builds only (wrong output): every window 16-aligned
-    if (plo || phi) v = load16_nt(ib + ((wp * in_stride + SKIP + wj) & ~15u));
-#elif defined(HY_X_TILE_PLAIN_LOADS)
-    if (plo || phi) v = load16u(ib + (wp * in_stride + SKIP + wj));
+__device__ __forceinline__ void glds16(const uint8_t* g, uint8_t* l) {   // LDS-DMA: l = wave base + lane * 16
+#ifdef HYOBFS_EMULATE
+    std::memcpy(l + 16 * (threadIdx.x & 63), g, 16);
 #else
-    if (plo || phi) v = load16_nt(ib + (wp * in_stride + SKIP + wj));
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
+                                     (__attribute__((address_space(3))) void*)l, 16, 0, HY_TILE_DMA_AUX);
 #endif
-    return f;
-}
-
-// XOR with the key words (and salts) from LDS, store the chunk.
-__device__ __forceinline__ void tile_store(uint8_t* __restrict__ ob, const uint64_t* s_key, const uint64_t* s_salt,
-                                           uint32_t f, uint32_t x, u128 v) {
-    if (!(f & (kTcVlo | kTcVhi))) return;
-    const uint32_t ki = f & 0xFFu;
-    const uint64_t k0 = s_key[ki], k1 = s_key[ki + 1];
-    const uint64_t wlo = (uint64_t)v, whi = (uint64_t)(v >> 64);
-    uint64_t lo = ((f & kTcLoFromHi) ? whi : wlo) ^ k0;
-    uint64_t hi = ((f & kTcHiFromLo) ? wlo : whi) ^ k1;
-    if (f & (kTcSlo | kTcShi)) {
-        const uint64_t sv = s_salt[(f >> 8) & 15u];
-        if (f & kTcSlo) lo = sv;
-        if (f & kTcShi) hi = sv;
-    }
-    if ((f & (kTcVlo | kTcVhi)) == (kTcVlo | kTcVhi))
-#ifdef HY_X_TILE_PLAIN_STORES
-        __builtin_memcpy(ob + x, &lo, 8), __builtin_memcpy(ob + x + 8, &hi, 8);
-#else
-        store16_global(ob + x, lo, hi);
-#endif
-    else if (f & kTcVlo)
-        store8_global(ob + x, lo);
-    else
-        store8_global(ob + x + 8, hi);
 }
 
 template <bool OBF, int SW>
 __global__ __launch_bounds__(256, HY_TILE_MIN_WAVES) void salamander_tile_kernel(BatchParams B, KeyParams K,
                                                                                   TileParams T) {
+    constexpr uint32_t SALT = OBF ? 8u : 0u;   // salt bytes in front of the output payload
+    constexpr uint32_t SKIP = OBF ? 0u : 8u;   // salt bytes in front of the input payload
+#ifdef HYOBFS_EMULATE
+    uint8_t* s_in = hyemu_dyn_lds();
+#else
+    extern __shared__ __attribute__((aligned(16))) uint8_t s_in[];   // the tile's input range
+#endif
     __shared__ uint64_t s_key[kTileMaxD * 8];   // each key twice: word w and w + 4 equal
     __shared__ uint64_t s_salt[kTileMaxD];
+    constexpr int U = kTSU;
 
     const uint32_t tid = threadIdx.x, lane = tid & 63;
     const uint32_t wid = uni32(tid >> 6);
@@ -356,31 +290,71 @@ __global__ __launch_bounds__(256, HY_TILE_MIN_WAVES) void salamander_tile_kernel
             if (B.out_len) B.out_len[p0 + lane] = W;
         }
         if (B.out_total && lane == 0) atomicAdd(B.out_total, (unsigned long long)nt * W);
-#ifndef HY_X_TILE_NOBAR
-        hy_lds_barrier();
-#endif
-        return;
+    } else {
+        // ---- waves 1-3: the tile's input range (16 * in_stride bytes at most, 16-aligned)
+        // into LDS, 1 KiB per instruction, nothing held in registers
+        const uint32_t in_end = (nt - 1) * in_stride + T.LI;
+        const uint32_t nfull = in_end >> 4;
+        for (uint32_t i = wid - 1; i * 64u < nfull; i += 3) {
+            const uint32_t ch = i * 64u + lane;
+            if (ch < nfull) glds16(ib + 16u * ch, s_in + 1024u * i);
+        }
+        if ((in_end & 15u) && wid == 3 && lane == 0)   // an 8-byte tail (inputs end on 8-byte boundaries)
+            *reinterpret_cast<uint64_t*>(s_in + 16u * nfull) = load8_nt(ib + 16u * nfull);
     }
+    __syncthreads();   // every wave's LDS-DMA has landed (vmcnt(0)), the keys are published
 
-    // ---- the three data waves: 1 KiB of output per wave instruction, kTU chunks
-    // per thread in flight; the first pass's loads are issued before the barrier
-    // that publishes the keys, so they overlap the hash
-    constexpr uint32_t kPass = 192u * kTU;      // chunks per pass
-    const uint32_t dt = tid - 64u;
+    // ---- every thread: compose its output chunks from LDS, 1 KiB per wave instruction
     uint8_t* __restrict__ ob = B.out + p0 * S;
     const uint32_t nch = (tbytes + 15u) >> 4;
-    for (uint32_t c0 = 0; c0 < nch; c0 += kPass) {
-        u128 v[kTU];
-        uint32_t tc[kTU];
+    for (uint32_t c0 = 0; c0 < nch; c0 += 256u * U) {
+        uint64_t lo[U], hi[U];
+        uint32_t st[U];   // bit 0 low half written, bit 1 high half written
 #pragma unroll
-        for (int u = 0; u < kTU; ++u)
-            tc[u] = tile_chunk<OBF>(ib, in_stride, S, W, T.invS, nt, tbytes, (c0 + (uint32_t)u * 192u + dt) << 4, v[u]);
-#ifndef HY_X_TILE_NOBAR   // (ablation builds only: keys not waited for, wrong output)
-        if (c0 == 0) hy_lds_barrier();
-#endif
+        for (int u = 0; u < U; ++u) {
+            const uint32_t c = c0 + (uint32_t)u * 256u + tid, x = c << 4;
+            st[u] = 0;
+            lo[u] = hi[u] = 0;
+            if (c >= nch) continue;
+            uint32_t p = (uint32_t)((float)x * T.invS);
+            int32_t r = (int32_t)(x - p * S);
+            if (r < 0) {
+                --p;
+                r += (int32_t)S;
+            } else if (r >= (int32_t)S) {
+                ++p;
+                r -= (int32_t)S;
+            }
+            uint32_t r2 = (uint32_t)r + 8u, p2 = p;
+            if (r2 >= S) {
+                r2 -= S;
+                ++p2;
+            }
+            const bool vlo = (uint32_t)r < W, vhi = p2 < nt && r2 < W;
+            const bool slo = OBF && (uint32_t)r < 8u, shi = OBF && r2 < 8u;
+            const uint32_t jlo = (uint32_t)r - SALT, jhi = r2 - SALT;
+            const uint32_t alo = p * in_stride + SKIP + jlo, ahi = p2 * in_stride + SKIP + jhi;
+            if (vlo && !slo && vhi && !shi && p2 == p) {   // inside one payload: two words, one key pair
+                const uint64_t* d = reinterpret_cast<const uint64_t*>(s_in + alo);
+                const uint32_t ki = p * 8u + ((jlo >> 3) & 3u);
+                lo[u] = d[0] ^ s_key[ki];
+                hi[u] = d[1] ^ s_key[ki + 1];
+            } else {
+                if (vlo) lo[u] = slo ? s_salt[p] : *reinterpret_cast<const uint64_t*>(s_in + alo) ^ s_key[p * 8u + ((jlo >> 3) & 3u)];
+                if (vhi) hi[u] = shi ? s_salt[p2] : *reinterpret_cast<const uint64_t*>(s_in + ahi) ^ s_key[p2 * 8u + ((jhi >> 3) & 3u)];
+            }
+            st[u] = (vlo ? 1u : 0u) | (vhi ? 2u : 0u);
+        }
 #pragma unroll
-        for (int u = 0; u < kTU; ++u)
-            tile_store(ob, s_key, s_salt, tc[u], (c0 + (uint32_t)u * 192u + dt) << 4, v[u]);
+        for (int u = 0; u < U; ++u) {
+            const uint32_t x = (c0 + (uint32_t)u * 256u + tid) << 4;
+            if (st[u] == 3u)
+                store16_global(ob + x, lo[u], hi[u]);
+            else if (st[u] == 1u)
+                store8_global(ob + x, lo[u]);
+            else if (st[u] == 2u)
+                store8_global(ob + x + 8, hi[u]);
+        }
     }
 }
 
@@ -396,13 +370,15 @@ inline bool tile_params(const BatchParams& b, TileParams& T) {
     if (L > kMaxDatagram || L < (OBF ? 16u : 24u)) return false;
     if ((L | b.out_stride | b.in_stride | reinterpret_cast<uintptr_t>(b.in)) & 7u) return false;
     if (b.in_stride > 0xFFFFFFFFull / kTileMaxD) return false;
+    // the staged input range: 16-aligned (LDS-DMA moves 16-byte chunks), at most 64 KiB of LDS
+    if ((reinterpret_cast<uintptr_t>(b.in) & 15u) || b.in_stride > 4096 || L > 4096) return false;
     const uint64_t W = OBF ? L + 8 : L - 8, S = b.out_stride;
     if ((b.pkt_cap && W > b.pkt_cap) || W > S) return false;
     if ((b.n - 1) * S + W > b.out_cap) return false;
-    if (!OBF && S == W && (W & 15u)) return false;
     if (S > kMaxTileSlot) return false;   // tile-local offsets stay 32-bit, float estimate exact enough
     T.S = (uint32_t)S;
     T.W = (uint32_t)W;
+    T.LI = (uint32_t)L;
     T.invS = 1.0f / (float)S;
     return true;
 }
@@ -410,7 +386,10 @@ inline bool tile_params(const BatchParams& b, TileParams& T) {
 template <bool OBF, int SW>
 void launch_tile_sw(const BatchParams& b, const KeyParams& k, const TileParams& T, hipStream_t s) {
     const uint64_t blocks = div_up(b.n, kTileMaxD);
-    hipLaunchKernelGGL((salamander_tile_kernel<OBF, SW>), dim3((uint32_t)blocks), dim3(256), 0, s, b, k, T);
+    // dynamic LDS: the longest tile input range, 15 strides plus one datagram (in_stride may be
+    // smaller than the length, e.g. 0 for one datagram)
+    const uint32_t shm = (uint32_t)(((kTileMaxD - 1) * b.in_stride + T.LI + 15) & ~15ull);
+    hipLaunchKernelGGL((salamander_tile_kernel<OBF, SW>), dim3((uint32_t)blocks), dim3(256), shm, s, b, k, T);
 }
 
 }  // namespace hyobfs

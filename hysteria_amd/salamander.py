@@ -102,8 +102,8 @@ def _make_batch(*, inp, n, in_off=None, in_stride=0, in_len=None, len_uniform=0,
 class SalamanderObfuscator:
     """A Salamander obfuscator bound to one MI355X (HIP device ``device``)."""
 
-    def __init__(self, psk: bytes, device: int = 0):
-        lib = _lib.load()
+    def __init__(self, psk: bytes, device: int = 0, lib_path: str | None = None):
+        lib = _lib.load(lib_path) if lib_path else _lib.load()
         psk = bytes(psk)
         if len(psk) < SM_PSK_MIN_LEN:
             raise PSKTooShortError()
@@ -258,6 +258,11 @@ def device_count() -> int:
 
 def workspace_size(n: int) -> int:
     return _lib.load().hyobfs_batch_workspace_size(n)
+
+
+def build_id() -> str:
+    """Kernel-source hash the loaded libhyobfs.so was built from (scripts/src_sha.py)."""
+    return _lib.load().hyobfs_build_id().decode()
 
 
 # ------------------------------------------------------------- synthetic inputs

@@ -76,6 +76,10 @@ typedef struct hyobfs_salamander hyobfs_salamander; /* opaque context */
 
 /* ------------------------------------------------------------------ basics */
 int hyobfs_abi_version(void);
+/* sha256 (16 hex digits) of the kernel sources this library was built from
+   (scripts/src_sha.py); "unknown" for builds outside the Makefile.  bench.py
+   uses committed PMC traffic figures only when they match it. */
+const char* hyobfs_build_id(void);
 const char* hyobfs_status_string(int status);
 /* number of HIP devices visible to this process (0 when none) */
 int hyobfs_device_count(void);

@@ -14,8 +14,8 @@ from bench import kernel_src_sha  # noqa: E402
 
 root, wl, src, dst = sys.argv[1:5]
 label = sys.argv[5] if len(sys.argv) > 5 else root
-MAIN = {True: re.compile(r"salamander_(uniform_kernel|wave_kernel|kernel)<true"),
-        False: re.compile(r"salamander_(uniform_kernel|wave_kernel|kernel)<false")}
+MAIN = {True: re.compile(r"salamander_(tile_kernel|wave_kernel)<true"),
+        False: re.compile(r"salamander_(tile_kernel|wave_kernel)<false")}
 
 
 def per_dispatch(counter, obf):

@@ -60,6 +60,7 @@ struct hipDeviceProp_t {
 
 namespace hyemu {
 struct Ctx {
+    std::unique_ptr<uint8_t[]> dyn;   // the block's dynamic LDS (exactly the launch's shmem bytes: ASan-checked)
     std::barrier<>* block = nullptr;
     std::barrier<>* wave[16] = {};
     uint64_t slots[1024];
@@ -92,12 +93,14 @@ inline void wave_sync() { g_ctx.wave[(int)t_thread.x >> 6]->arrive_and_wait(); }
 inline std::mutex g_launch_mu;   // the state above is global: one launch at a time
 
 template <class F>
-inline void launch(dim3 grid, dim3 block, F&& body) {
+inline void launch(dim3 grid, dim3 block, size_t shmem, F&& body) {
     std::lock_guard<std::mutex> lk(g_launch_mu);
     g_grid = grid;
     g_blockdim = block;
     const uint32_t nt = block.x;
     for (uint32_t b = 0; b < grid.x; ++b) {
+        g_ctx.dyn.reset(new uint8_t[shmem ? shmem : 1]);
+        std::memset(g_ctx.dyn.get(), 0xCD, shmem ? shmem : 1);
         std::barrier<> bar((std::ptrdiff_t)nt);
         std::vector<std::unique_ptr<std::barrier<>>> waves;
         for (uint32_t w = 0; w < (nt + 63) / 64; ++w) {
@@ -188,7 +191,8 @@ inline unsigned long long atomicAdd(unsigned long long* p, unsigned long long v)
 }
 
 #define hipLaunchKernelGGL(kernel, grid, block, shmem, stream, ...) \
-    hyemu::launch(dim3(grid), dim3(block), [&] { kernel(__VA_ARGS__); })
+    hyemu::launch(dim3(grid), dim3(block), (size_t)(shmem), [&] { kernel(__VA_ARGS__); })
+inline uint8_t* hyemu_dyn_lds() { return hyemu::g_ctx.dyn.get(); }
 
 // ---- runtime API subset
 inline hipError_t hipGetLastError() { return hipSuccess; }

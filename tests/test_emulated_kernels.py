@@ -128,17 +128,19 @@ RUN_CASES = [
 
 
 # The tile kernel (salamander_tile.h): slotted batches whose region edges are all
-# multiples of 8.  Dense slots of 8 mod 16 (obfuscate 1200 -> 1208) and 0 mod 16,
-# gapped slots (gap bytes untouched), input strides with padding, partial last
-# tiles, large slots (fewer datagrams per tile), every salt-word position of the
-# PSK (lengths 4..127, including the two-block case 121..127), and layouts that
-# do not qualify (odd lengths, deobfuscate into dense slots of 8 mod 16: the wave kernel).
+# multiples of 8.  Dense slots of 8 mod 16 (obfuscate 1200 -> 1208, deobfuscate
+# 1216 -> 1208) and 0 mod 16, gapped slots (gap bytes untouched), input strides with
+# padding, partial last tiles, slots needing several compose passes (9000 B), every
+# salt-word position of the PSK (lengths 4..127, including the two-block case
+# 121..127), and layouts that do not qualify (odd lengths, inputs over 4 KiB: the
+# wave kernel).
 TILE_CASES = [
     ("uniform", "257 1200 1"), ("uniform", "256 1200 0"), ("uniform", "301 1192 1"), ("uniform", "301 1192 0"),
     ("uniform", "33 16 1"), ("uniform", "33 24 0"), ("uniform", "300 17 1"), ("uniform", "99 1201 0"),
     ("slotted", "70 1200 1 24 8 16"), ("slotted", "70 1208 0 8 0 16"), ("slotted", "45 2040 1 0 16 9"),
     ("slotted", "37 4096 0 16 0 31"), ("slotted", "21 9000 1 0 0 16"), ("slotted", "40 64 1 0 0 4"),
-    ("slotted", "40 64 0 0 24 5"), ("slotted", "23 100 1 4 4 16"),
+    ("slotted", "40 64 0 0 24 5"), ("slotted", "23 100 1 4 4 16"), ("slotted", "30 1216 0 0 0 16"),
+    ("slotted", "17 4096 1 8 0 16"), ("slotted", "17 4104 1 0 0 16"),
 ] + [("slotted", f"18 {L} 1 {pad} 0 {k}") for k, L, pad in
      [(4, 40, 0), (8, 48, 8), (12, 136, 0), (20, 200, 16), (60, 96, 0), (100, 1000, 8), (119, 512, 0),
       (120, 256, 0), (121, 256, 8), (124, 512, 0), (127, 264, 0), (128, 64, 0), (300, 1200, 0)]]
