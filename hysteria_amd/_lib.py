@@ -125,6 +125,8 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         "hyobfs_conn_write_batch": (i32, [vp, vp, u32]),
         "hyobfs_conn_set_coalescing": (i32, [vp, u32, u32]),
         "hyobfs_conn_flush": (i32, [vp]),
+        "hyobfs_conn_set_read_deadline": (i32, [vp, ctypes.c_int64]),
+        "hyobfs_conn_set_write_deadline": (i32, [vp, ctypes.c_int64]),
         "hyobfs_conn_stats": (i32, [vp, ctypes.POINTER(ctypes.c_uint64)]),
         "hyobfs_synth_stream": (i32, [vp, u64, u64, u64, vp]),
         "hyobfs_synth_u64": (i32, [vp, u64, u64, u64, vp]),

@@ -12,7 +12,9 @@ reference (Go)                             here
 ``WriteTo(p, addr)`` (conn.go:90-99)       ``write_to(p, addr) -> len(p)``
 ``Close()`` (conn.go:101-103)              ``close()`` (closes the socket)
 ``LocalAddr()`` (conn.go:105-107)          ``local_addr()``
-``Set{,Read,Write}Deadline``               ``settimeout(seconds)`` (SO_RCVTIMEO/SO_SNDTIMEO)
+``Set{,Read,Write}Deadline``               ``set_deadline(t)`` / ``set_read_deadline(t)`` /
+(conn.go:109-119)                          ``set_write_deadline(t)`` (absolute ``time.time()``
+                                           seconds, None = none), or ``settimeout(seconds)``
 ``SetReadBuffer`` / ``SetWriteBuffer``     ``set_read_buffer`` / ``set_write_buffer``
 (new) batched receive / send               ``read_batch(n)`` / ``write_batch(msgs)``
 (new) coalescing per-datagram calls        ``set_coalescing(max_batch, max_wait_us)``,
@@ -133,6 +135,21 @@ class SalamanderPacketConn:
         self._sock.setsockopt(socket.SOL_SOCKET, socket.SO_RCVTIMEO, tv)
         self._sock.setsockopt(socket.SOL_SOCKET, socket.SO_SNDTIMEO, tv)
         self._timeout = seconds
+
+    def set_read_deadline(self, t: float | None) -> None:
+        """SetReadDeadline: absolute time (time.time() seconds) or None; applies to blocked reads too."""
+        check(self._lib.hyobfs_conn_set_read_deadline(self._h, 0 if t is None else max(1, int(t * 1e9))),
+              "set_read_deadline")
+
+    def set_write_deadline(self, t: float | None) -> None:
+        """SetWriteDeadline: absolute time (time.time() seconds) or None."""
+        check(self._lib.hyobfs_conn_set_write_deadline(self._h, 0 if t is None else max(1, int(t * 1e9))),
+              "set_write_deadline")
+
+    def set_deadline(self, t: float | None) -> None:
+        """SetDeadline: both deadlines."""
+        self.set_read_deadline(t)
+        self.set_write_deadline(t)
 
     def set_read_buffer(self, nbytes: int) -> None:
         self._sock.setsockopt(socket.SOL_SOCKET, socket.SO_RCVBUF, nbytes)

@@ -106,8 +106,31 @@ class Spin {
 
 }  // namespace
 
+int64_t realtime_ns() {
+    return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::system_clock::now().time_since_epoch())
+        .count();
+}
+
+// Waits on cv until pred() or the absolute deadline dl (0: none) passes; false on the deadline.
+template <class Pred>
+static bool wait_deadline(std::condition_variable& cv, std::unique_lock<std::mutex>& lk, const std::atomic<int64_t>& dl,
+                          Pred pred) {
+    for (;;) {
+        if (pred()) return true;
+        const int64_t d = dl.load(std::memory_order_acquire);
+        if (d == 0) {
+            cv.wait(lk);   // a deadline set later pokes the condition variable
+            continue;
+        }
+        const int64_t now = realtime_ns();
+        if (now >= d) return pred();
+        cv.wait_for(lk, std::chrono::nanoseconds(d - now));
+    }
+}
+
 struct Coalescer {
     int fd = -1;
+    const Deadlines* dl = nullptr;
     hyobfs_salamander* ctx = nullptr;
     uint32_t max_batch = 0;
     std::chrono::microseconds max_wait{0};
@@ -308,10 +331,12 @@ void Coalescer::read_loop() {
     }
 }
 
-Coalescer* coalescer_new(int fd, hyobfs_salamander* ctx, uint32_t max_batch, uint32_t max_wait_us) {
+Coalescer* coalescer_new(int fd, hyobfs_salamander* ctx, uint32_t max_batch, uint32_t max_wait_us,
+                         const Deadlines* dl) {
     auto* q = new (std::nothrow) Coalescer();
     if (!q) return nullptr;
     q->fd = fd;
+    q->dl = dl;
     q->ctx = ctx;
     q->max_batch = max_batch;
     q->max_wait = std::chrono::microseconds(max_wait_us);
@@ -379,6 +404,10 @@ int64_t coalescer_write(Coalescer* q, const uint8_t* p, size_t len, const void* 
         errno = EBADF;
         return -1;
     }
+    if (const int64_t d = q->dl->write.load(std::memory_order_acquire); d && realtime_ns() >= d) {
+        errno = EAGAIN;   // the write deadline has passed
+        return -1;
+    }
     if (q->tx_err_pending.load(std::memory_order_relaxed)) {   // an earlier datagram's send failed
         const int e = q->tx_err_pending.exchange(0);
         if (e) {
@@ -400,7 +429,7 @@ int64_t coalescer_write(Coalescer* q, const uint8_t* p, size_t len, const void* 
         q->spin.unlock();
         std::unique_lock<std::mutex> lk(q->tx_mu);
         q->cv_flush.notify_one();   // the filling batch is full
-        q->cv_space.wait(lk, [&] {
+        const bool ok = wait_deadline(q->cv_space, lk, q->dl->write, [&] {
             q->spin.lock();
             const bool s = q->has_space();
             q->spin.unlock();
@@ -408,6 +437,10 @@ int64_t coalescer_write(Coalescer* q, const uint8_t* p, size_t len, const void* 
         });
         if (q->stop) {
             errno = EBADF;
+            return -1;
+        }
+        if (!ok) {   // SetWriteDeadline passed while both batches were busy
+            errno = EAGAIN;
             return -1;
         }
     }
@@ -429,7 +462,9 @@ int64_t coalescer_write(Coalescer* q, const uint8_t* p, size_t len, const void* 
 
 int64_t coalescer_read(Coalescer* q, uint8_t* p, size_t cap, void* addr, uint32_t* addrlen) {
     CallerGuard g(q);
-    // SetReadDeadline: SO_RCVTIMEO read once, one absolute deadline for the whole call
+    // SetReadDeadline: the connection's absolute read deadline if one is set
+    // (re-read whenever it changes), else SO_RCVTIMEO read once, one absolute
+    // deadline for the whole call
     timeval tv{0, 0};
     socklen_t tl = sizeof tv;
     (void)getsockopt(q->fd, SOL_SOCKET, SO_RCVTIMEO, &tv, &tl);
@@ -451,10 +486,15 @@ int64_t coalescer_read(Coalescer* q, uint8_t* p, size_t cap, void* addr, uint32_
                     errno = EBADF;
                     return -1;
                 }
-                if (!timed) {
+                auto woken = [&] { return !q->ready.empty() || q->rx_err || q->stop; };
+                if (q->dl->read.load(std::memory_order_acquire)) {
+                    if (!wait_deadline(q->cv_ready, lk, q->dl->read, woken)) {
+                        errno = EAGAIN;
+                        return -1;
+                    }
+                } else if (!timed) {
                     q->cv_ready.wait(lk);
-                } else if (!q->cv_ready.wait_until(lk, deadline,
-                                                   [&] { return !q->ready.empty() || q->rx_err || q->stop; })) {
+                } else if (!q->cv_ready.wait_until(lk, deadline, woken)) {
                     errno = EAGAIN;
                     return -1;
                 }
@@ -486,6 +526,16 @@ int64_t coalescer_read(Coalescer* q, uint8_t* p, size_t cap, void* addr, uint32_
         }
         if (deliver) return n;
     }
+}
+
+void coalescer_poke(Coalescer* q) {
+    if (!q) return;
+    {
+        std::lock_guard<std::mutex> a(q->tx_mu);
+        std::lock_guard<std::mutex> b(q->rx_mu);
+    }
+    q->cv_space.notify_all();
+    q->cv_ready.notify_all();
 }
 
 int coalescer_flush(Coalescer* q) {

@@ -5,14 +5,26 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include <atomic>
+
 #include "../../include/hyobfs.h"
 
 namespace hyobfs {
 
 struct Coalescer;
 
+// Absolute deadlines of a connection (CLOCK_REALTIME ns since the epoch, 0 = none),
+// owned by the connection: SetReadDeadline / SetWriteDeadline.
+struct Deadlines {
+    std::atomic<int64_t> read{0}, write{0};
+};
+int64_t realtime_ns();
+
 // Starts the flusher and reader threads on fd.  nullptr on allocation failure.
-Coalescer* coalescer_new(int fd, hyobfs_salamander* ctx, uint32_t max_batch, uint32_t max_wait_us);
+Coalescer* coalescer_new(int fd, hyobfs_salamander* ctx, uint32_t max_batch, uint32_t max_wait_us,
+                         const Deadlines* dl);
+// Wakes blocked callers so they re-read the deadlines (after a change).
+void coalescer_poke(Coalescer* q);
 // Sends what was accepted, wakes blocked callers (-1, EBADF), stops the threads.
 void coalescer_stop(Coalescer* q);
 // coalescer_stop, then frees everything (not the fd) once no caller is inside.

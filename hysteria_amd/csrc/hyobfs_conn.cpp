@@ -6,6 +6,7 @@
 #include "conn_coalesce.h"
 
 #include <errno.h>
+#include <poll.h>
 #include <string.h>
 #include <sys/socket.h>
 #include <unistd.h>
@@ -60,6 +61,7 @@ struct hyobfs_conn {
     std::vector<iovec> riov, wiov;
     std::vector<sockaddr_storage> raddr;
     hyobfs::Coalescer* co = nullptr;       // set: per-datagram calls go through batches
+    hyobfs::Deadlines dl;                  // SetReadDeadline / SetWriteDeadline (absolute, 0 = none)
     std::atomic<bool> closing{false};      // Close() has begun: calls return -1, EBADF
     std::atomic<int> inflight{0};          // threads inside read_from / write_to / *_batch
 };
@@ -146,8 +148,26 @@ int64_t hyobfs_conn_read_from(hyobfs_conn* c, uint8_t* p, size_t cap, void* addr
     if (c->co) return hyobfs::coalescer_read(c->co, p, cap, addr, addrlen);
     for (;;) {
         std::lock_guard<std::mutex> lk(c->read_mu);
+        int flags = 0;
+        if (c->dl.read.load(std::memory_order_acquire)) {
+            // a read deadline: wait in slices of at most 50 ms, re-reading it (it
+            // may move while this call waits), then receive without blocking
+            for (;;) {
+                const int64_t d = c->dl.read.load(std::memory_order_acquire);
+                const int64_t left = d ? d - hyobfs::realtime_ns() : 50000000;
+                if (d && left <= 0) {
+                    errno = EAGAIN;
+                    return -1;
+                }
+                pollfd pf{c->fd, POLLIN, 0};
+                const int pr = poll(&pf, 1, (int)std::min<int64_t>(50, (left + 999999) / 1000000));
+                if (g.closed()) return -1;
+                if (pr > 0) break;
+            }
+            flags = MSG_DONTWAIT;
+        }
         socklen_t al = addrlen ? *addrlen : 0;
-        const ssize_t n = recvfrom(c->fd, c->read_buf, kBuf, 0, static_cast<sockaddr*>(addr), addr ? &al : nullptr);
+        const ssize_t n = recvfrom(c->fd, c->read_buf, kBuf, flags, static_cast<sockaddr*>(addr), addr ? &al : nullptr);
         if (addrlen) *addrlen = al;
         if (n <= 0 && g.closed()) return -1;   // woken by Close()
         if (n <= 0) return n;   // error or empty datagram: returned as is (:77-80)
@@ -167,6 +187,10 @@ int64_t hyobfs_conn_write_to(hyobfs_conn* c, const uint8_t* p, size_t len, const
     if (g.closed()) return -1;
     if (c->co) return hyobfs::coalescer_write(c->co, p, len, addr, addrlen);
     std::lock_guard<std::mutex> lk(c->write_mu);
+    if (const int64_t d = c->dl.write.load(std::memory_order_acquire); d && hyobfs::realtime_ns() >= d) {
+        errno = EAGAIN;   // SetWriteDeadline has passed
+        return -1;
+    }
     // Obfuscate into the 2048-byte writeBuf: 0 when len > 2040 (salamander.go:60-62)
     const size_t nn = hyobfs_salamander_obfuscate_auto(c->ctx, p, len, c->write_buf, kBuf);
     const ssize_t rc = sendto(c->fd, c->write_buf, nn, 0, static_cast<const sockaddr*>(addr), addrlen);
@@ -292,8 +316,22 @@ int hyobfs_conn_write_batch(hyobfs_conn* c, const hyobfs_dgram* msgs, uint32_t n
 
 int hyobfs_conn_set_coalescing(hyobfs_conn* c, uint32_t max_batch, uint32_t max_wait_us) {
     if (!c || c->co || max_batch == 0 || max_batch > (1u << 16)) return HYOBFS_ERR_INVALID;
-    c->co = hyobfs::coalescer_new(c->fd, c->ctx, max_batch, max_wait_us);
+    c->co = hyobfs::coalescer_new(c->fd, c->ctx, max_batch, max_wait_us, &c->dl);
     return c->co ? HYOBFS_OK : HYOBFS_ERR_NOMEM;
+}
+
+int hyobfs_conn_set_read_deadline(hyobfs_conn* c, int64_t unix_ns) {
+    if (!c || unix_ns < 0) return HYOBFS_ERR_INVALID;
+    c->dl.read.store(unix_ns, std::memory_order_release);
+    hyobfs::coalescer_poke(c->co);   // blocked reads re-read it (net.Conn: also currently-blocked calls)
+    return HYOBFS_OK;
+}
+
+int hyobfs_conn_set_write_deadline(hyobfs_conn* c, int64_t unix_ns) {
+    if (!c || unix_ns < 0) return HYOBFS_ERR_INVALID;
+    c->dl.write.store(unix_ns, std::memory_order_release);
+    hyobfs::coalescer_poke(c->co);
+    return HYOBFS_OK;
 }
 
 int hyobfs_conn_flush(hyobfs_conn* c) {

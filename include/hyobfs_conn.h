@@ -9,7 +9,8 @@
  *   (*obfsPacketConn).ReadFrom(p)        conn.go:73-88  hyobfs_conn_read_from
  *   (*obfsPacketConn).WriteTo(p, addr)   conn.go:90-99  hyobfs_conn_write_to
  *   (*obfsPacketConn).Close()            conn.go:101-103 hyobfs_conn_close
- *   LocalAddr / deadlines / Set*Buffer   conn.go:105-133 the caller keeps the fd
+ *   Set{Read,Write}Deadline              conn.go:109-119 hyobfs_conn_set_{read,write}_deadline
+ *   LocalAddr / Set*Buffer / SyscallConn conn.go:105-133 the caller keeps the fd
  *   (new) batched receive / send                        hyobfs_conn_read_batch / _write_batch
  *
  * Reference behaviour kept:
@@ -78,6 +79,15 @@ int hyobfs_conn_read_batch(hyobfs_conn* c, hyobfs_dgram* msgs, uint32_t n);
 /* Obfuscate and send n datagrams with one GPU batch.  Returns the count sent,
    or -1 with errno set. */
 int hyobfs_conn_write_batch(hyobfs_conn* c, const hyobfs_dgram* msgs, uint32_t n);
+
+/* SetReadDeadline / SetWriteDeadline (conn.go:109-119, net.Conn semantics): an
+   absolute CLOCK_REALTIME time in ns since the Unix epoch (Go: t.UnixNano()),
+   0 = no deadline.  It applies to future calls AND to calls blocked right now
+   (they re-read it); once passed, read_from / write_to return -1 with errno
+   EAGAIN (Go: os.ErrDeadlineExceeded).  A read deadline takes precedence over
+   the socket's SO_RCVTIMEO.  SetDeadline = both. */
+int hyobfs_conn_set_read_deadline(hyobfs_conn* c, int64_t unix_ns);
+int hyobfs_conn_set_write_deadline(hyobfs_conn* c, int64_t unix_ns);
 
 /* Coalescing mode (no reference counterpart: a throughput knob behind the
    unchanged per-datagram surface, conn.go:73-99).  After this call:

@@ -346,3 +346,69 @@ def run_lifecycle_scenarios(device: int = 0, n: int = 200, max_batch: int = 64, 
     finally:
         raw.close()
         oa.close()
+
+
+def run_deadline_scenarios(device: int = 0, max_batch: int = 16):
+    """SetReadDeadline / SetWriteDeadline (conn.go:109-119, net.Conn semantics) in
+    plain and coalescing mode: an idle read times out at its deadline; moving the
+    deadline into the past wakes a read that is blocked right now; clearing it
+    (None) lets reads block again; a passed write deadline fails write_to; data
+    that is there is read before the deadline matters."""
+    import threading
+    import time
+    oa = SalamanderObfuscator(PSK, device)
+    raw = _udp()
+    try:
+        for coalescing in (False, True):
+            c = SalamanderPacketConn(_udp(), oa, batch=max_batch)
+            if coalescing:
+                c.set_coalescing(max_batch, 100)
+            addr = c.local_addr()
+            # 1. an idle read ends at its deadline
+            t0 = time.time()
+            c.set_read_deadline(t0 + 0.3)
+            try:
+                c.read_from()
+                raise AssertionError("read did not time out")
+            except TimeoutError:
+                pass
+            dt = time.time() - t0
+            assert 0.25 <= dt < 5.0, (coalescing, dt)
+            # 2. a datagram that is there is read while the deadline is in the future
+            c.set_read_deadline(time.time() + 5.0)
+            raw.sendto(ref.obfuscate(PSK, b"hello", b"\x01" * 8, 13), addr)
+            assert c.read_from() == (b"hello", raw.getsockname())
+            # 3. a read blocked with no deadline wakes when the deadline moves into the past
+            c.set_read_deadline(None)
+            got = []
+
+            def blocked():
+                try:
+                    c.read_from()
+                    got.append("returned")
+                except TimeoutError:
+                    got.append("timeout")
+            th = threading.Thread(target=blocked)
+            th.start()
+            time.sleep(0.3)
+            assert th.is_alive(), "read returned without data or deadline"
+            c.set_read_deadline(time.time() - 1.0)
+            th.join(10)
+            assert not th.is_alive() and got == ["timeout"], (coalescing, got)
+            # 4. a passed write deadline fails the write; clearing it lets writes through
+            c.set_write_deadline(time.time() - 1.0)
+            try:
+                c.write_to(b"late", raw.getsockname())
+                raise AssertionError("write after the deadline succeeded")
+            except TimeoutError:
+                pass
+            c.set_deadline(None)
+            assert c.write_to(b"on time", raw.getsockname()) == 7
+            if coalescing:
+                c.flush()
+            wire, _ = raw.recvfrom(4096)
+            assert ref.deobfuscate(PSK, wire) == b"on time"
+            c.close()
+    finally:
+        raw.close()
+        oa.close()

@@ -297,6 +297,10 @@ if __name__ == "__main__":
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         from conn_cases import run_lifecycle_scenarios
         run_lifecycle_scenarios(n=args[0], max_batch=args[1])
+    elif which == "deadline":
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        from conn_cases import run_deadline_scenarios
+        run_deadline_scenarios()
     elif which == "far":
         case_slotted_far(args[0], args[1], args[2], bool(args[3]))
     elif which == "ragged":

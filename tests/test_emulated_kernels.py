@@ -36,7 +36,7 @@ def emu_lib():
 SPECS = {
     "test_emulated_tile_kernel": lambda p: (p["which"], p["args"], {"HYOBFS_KERNEL": "tile", "HYEMU_CUS": "2"}),
     "test_emulated_wave_kernel_forced": lambda p: None if p["which"] in ("conn", "host", "coalesce", "quic",
-                                                                         "lifecycle") else (
+                                                                         "lifecycle", "deadline") else (
         p["which"], p["args"], {"HYEMU_CUS": p["cus"], "HYOBFS_KERNEL": "wave"}),
     "test_emulated_wave_kernel_run_lengths": lambda p: (
         p["which"], p["args"], {"HYOBFS_RUN_LOG2": p["run_log2"], "HYOBFS_KERNEL": "wave"}),
@@ -102,6 +102,7 @@ CASES = [
     ("conn", "64 120", "2"),             # UDP loopback through the conn wrapper (conn.go)
     ("coalesce", "8 150 4 32", "2"),     # many threads on one coalescing conn (hyobfs_conn_set_coalescing)
     ("lifecycle", "60 16", "2"),         # close() flushes, wakes blocked callers; deferred send errors
+    ("deadline", "", "2"),               # Set{Read,Write}Deadline, both modes
     ("far", "200 300 15 1", "8"),        # workgroup bases beyond 2^31
     ("far", "200 300 15 0", "8"),
     ("gecko", "40 7", "2"),              # Gecko frame encode + parse kernels (gecko.hip), aligned sweep
@@ -167,7 +168,7 @@ def test_emulated_wave_kernel_packed_run_lengths(emu_lib, which, args, run_log2)
 @pytest.mark.parametrize("which,args,cus", CASES)
 def test_emulated_wave_kernel_forced(emu_lib, which, args, cus):
     """The wave-group kernel (HYOBFS_KERNEL=wave) on every case, also where AUTO runs the tile kernel."""
-    if which in ("conn", "host", "coalesce", "quic", "lifecycle"):
+    if which in ("conn", "host", "coalesce", "quic", "lifecycle", "deadline"):
         pytest.skip("kernel-independent host paths run once, under the default kernel")
     _run(emu_lib, which, args, {"HYEMU_CUS": cus, "HYOBFS_KERNEL": "wave"})
 

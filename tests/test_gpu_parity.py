@@ -213,12 +213,14 @@ def test_config4_shard7_8M_x_1200_digest_and_roundtrip(gpu, golden):
         assert torch.equal(back, inp)
 
 
-def test_concurrent_packed_batches_one_context(gpu, coracle):
+@pytest.mark.parametrize("kernel", ["auto", "wave"])
+def test_concurrent_batches_one_context(gpu, coracle, kernel):
     """hyobfs.h promises a context may be used from several threads: two host
-    threads, each on its own stream, submit 50 packed ragged batches of changing
-    sizes through ONE context with no caller workspace (the context's per-stream
-    scratch, grown while the other thread's kernels run).  Every output against
-    the oracle."""
+    threads, each on its own stream, submit 50 batches through ONE context --
+    packed ragged batches of changing sizes with no caller workspace (the
+    context's pooled scratch, allocated and freed on each stream while the other
+    thread's kernels run) alternating with uniform slotted 1200-byte batches
+    (the tile kernel under AUTO).  Every output against the oracle."""
     import threading
     import torch
     import hysteria_amd
@@ -233,17 +235,26 @@ def test_concurrent_packed_batches_one_context(gpu, coracle):
         exp, _, _, _ = coracle.batch(True, PSK, n, h_inp, in_off=h_off[:n], in_len=h_lens[:n], salts=h_salts[:n],
                                      out_cap=cap)
         want[n] = exp
+    L, nu = 1200, 4000   # the uniform slotted batch: the first nu * L bytes of the same input
+    want_u, _, _, _ = coracle.batch(True, PSK, nu, h_inp, in_stride=L, len_uniform=L, salts=h_salts[:nu],
+                                    out_cap=nu * (L + 8), out_stride=L + 8)
     results = {0: [], 1: []}
     errors = []
     with hysteria_amd.SalamanderObfuscator(PSK, 0) as o:
-        o.set_kernel("persistent")   # packed ragged: the kernel behind the tile-sum scratch
+        o.set_kernel(kernel)
 
         def worker(t):
             try:
                 s = torch.cuda.Stream(device=gpu)
                 with torch.cuda.stream(s):
                     for i in range(50):
-                        n = sizes[t][i % 5]
+                        if i % 2:
+                            out = torch.empty(nu * (L + 8), dtype=torch.uint8, device=gpu)
+                            o.obfuscate_batch(inp, nu, in_stride=L, len_uniform=L, salts=salts, out=out,
+                                              out_stride=L + 8, stream=s)
+                            results[t].append((-1, out))
+                            continue
+                        n = sizes[t][(i // 2) % 5]
                         cap = want[n].size
                         out = torch.empty(cap, dtype=torch.uint8, device=gpu)
                         o.obfuscate_batch(inp, n, in_off=in_off, in_len=lens, salts=salts, out=out, out_cap=cap,
@@ -263,7 +274,38 @@ def test_concurrent_packed_batches_one_context(gpu, coracle):
     for t in (0, 1):
         assert len(results[t]) == 50
         for i, (n, out) in enumerate(results[t]):
-            assert np.array_equal(_host(out), want[n]), (t, i, n)
+            assert np.array_equal(_host(out), want_u if n < 0 else want[n]), (t, i, n)
+
+
+def test_pooled_scratch_bounded_over_many_streams(gpu):
+    """The context's packed-batch scratch (no caller workspace) comes from a pool,
+    allocated and freed in stream order: cycling 100 short-lived streams through
+    one context must not grow device memory (round 2 kept one buffer per stream
+    until the context died)."""
+    import torch
+    import hysteria_amd
+    n = 200_000
+    lens, in_off, inp, salts, total_in = _bimodal(gpu, n)
+    cap = total_in + 8 * n
+    out = torch.empty(cap, dtype=torch.uint8, device=gpu)
+    with hysteria_amd.SalamanderObfuscator(PSK, 0) as o:
+        def one(s):
+            o.obfuscate_batch(inp, n, in_off=in_off, in_len=lens, salts=salts, out=out, out_cap=cap, stream=s)
+            s.synchronize()
+        for _ in range(3):   # warm the pool
+            one(torch.cuda.Stream(device=gpu))
+        torch.cuda.synchronize()
+        free0 = torch.cuda.mem_get_info(gpu)[0]
+        for _ in range(100):
+            one(torch.cuda.Stream(device=gpu))
+        torch.cuda.synchronize()
+        free1 = torch.cuda.mem_get_info(gpu)[0]
+        # one batch's scratch is 8 B per 256 datagrams; 100 kept buffers would be
+        # 100 x that plus allocation granularity: allow 64 MiB of noise
+        assert free0 - free1 < (64 << 20), (free0, free1)
+        ref_out = out.clone()
+        one(torch.cuda.Stream(device=gpu))
+        assert torch.equal(out, ref_out)
 
 
 def _bimodal(gpu, n):
@@ -541,6 +583,14 @@ def test_packet_conn_lifecycle(gpu):
     sys.path.insert(0, os.path.dirname(__file__))
     from conn_cases import run_lifecycle_scenarios
     run_lifecycle_scenarios(device=0)
+
+
+def test_packet_conn_deadlines(gpu):
+    """Set{Read,Write}Deadline (conn.go:109-119) in plain and coalescing mode."""
+    import sys, os
+    sys.path.insert(0, os.path.dirname(__file__))
+    from conn_cases import run_deadline_scenarios
+    run_deadline_scenarios(device=0)
 
 
 def test_packet_conn_coalescing_loopback(gpu):
