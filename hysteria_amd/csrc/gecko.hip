@@ -7,9 +7,9 @@
 // salt); a wave scan numbers the group's 16-byte plaintext windows, and the 64
 // lanes sweep the interior ones, several per lane in flight (loads first, then
 // stores), each lane walking its window's frame forward through the LDS scan: a window
-// inside the chunk is one unaligned 16-byte load, one inside the padding is two
-// SplitMix64 words (pad byte at plaintext position q is stream byte f*2048 + q),
-// each leaves as one 16-byte store.  Then lane l merges frame l's few edge windows
+// inside the chunk is one unaligned 16-byte load, one inside the padding is one
+// column of a ChaCha8 keystream block (keyed per batch; four lanes per block, see
+// gk_ks_quad), each leaves as one 16-byte store.  Then lane l merges frame l's few edge windows
 // (header, padding/chunk seam, frame end) under byte masks; keeping them out of
 // the sweep keeps its lanes on the same path.  Lane l hashes frame l's key
 // (BLAKE2b-256, salamander_device.h) in registers in step 1, so the hash overlaps
@@ -22,12 +22,6 @@
 #include "../../include/hyobfs_gecko.h"
 
 namespace hyobfs {
-
-__device__ __forceinline__ uint64_t gk_mix64(uint64_t z) {   // SplitMix64 finaliser
-    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
-    z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
-    return z ^ (z >> 31);
-}
 
 typedef unsigned __int128 gk_u128;
 __device__ __forceinline__ gk_u128 gk_load16u(const uint8_t* p) {   // any alignment
@@ -58,18 +52,96 @@ struct GeckoGroup {             // one wave's 64 frames, in LDS
     gk_u128 key[128];           // the frame's key, two halves (aligned path: rotated to the wire phase)
 };
 
-// Pad stream bytes at plaintext [p0, p0 + 16) of frame f (p0 may be negative:
-// those bytes are garbage, masked by the caller): stream byte f*2048 + q is
-// byte q%8 of SplitMix64 output (f*2048 + q) / 8.
-__device__ __forceinline__ gk_u128 gk_pad_at(uint64_t seed, uint64_t f, int32_t p0) {
-    const int64_t sidx = (int64_t)(f * HYOBFS_GECKO_BUFFER_SIZE) + p0;
-    const uint64_t w = (uint64_t)(sidx >> 3);
-    const uint32_t sh = (uint32_t)(sidx & 7) * 8;
-    const uint64_t z = seed + (w + 1) * 0x9e3779b97f4a7c15ull;
-    const uint64_t w0 = gk_mix64(z), w1 = gk_mix64(z + 0x9e3779b97f4a7c15ull),
-                   w2 = gk_mix64(z + 2 * 0x9e3779b97f4a7c15ull);
-    const gk_u128 lo = (gk_u128)w1 << 64 | w0;
-    return sh ? (lo >> sh) | ((gk_u128)w2 << (128 - sh)) : lo;
+// ---- padding keystream (include/hyobfs_gecko.h): ChaCha, 8 rounds, RFC 8439 block
+// (constants, 8 key words, 32-bit counter, 3 nonce words), each 64-byte block's
+// bytes in column order: keystream bytes 64 blk + 16 c .. + 15 are state words c,
+// c + 4, c + 8, c + 12.  Pad byte j of frame i is keystream byte out_off[i] + 13 + j.
+// Column order lets four lanes compute one block, a column each, with no transpose.
+#ifndef HY_GK_PAD_ROUNDS
+#define HY_GK_PAD_ROUNDS 8
+#endif
+struct GkPad {
+    uint32_t k[8], n[3];
+};
+__device__ __forceinline__ GkPad gk_pad_params(const hyobfs_gecko_batch& B) {
+    GkPad P;
+    __builtin_memcpy(P.k, B.pad_key, 32);
+    __builtin_memcpy(P.n, B.pad_nonce, 12);
+    return P;
+}
+__device__ __forceinline__ uint32_t gk_rotl(uint32_t x, int n) { return __builtin_amdgcn_alignbit(x, x, 32 - n); }
+#define GK_QR(a, b, c, d)         \
+    do {                          \
+        a += b;                   \
+        d = gk_rotl(d ^ a, 16);   \
+        c += d;                   \
+        b = gk_rotl(b ^ c, 12);   \
+        a += b;                   \
+        d = gk_rotl(d ^ a, 8);    \
+        c += d;                   \
+        b = gk_rotl(b ^ c, 7);    \
+    } while (0)
+constexpr uint32_t kChaC0 = 0x61707865u, kChaC1 = 0x3320646Eu, kChaC2 = 0x79622D32u, kChaC3 = 0x6B206574u;
+__device__ __forceinline__ uint32_t gk_sel4(uint32_t x0, uint32_t x1, uint32_t x2, uint32_t x3, uint32_t i) {
+    return i == 0 ? x0 : i == 1 ? x1 : i == 2 ? x2 : x3;
+}
+
+// Column qi (= this lane's place in its quad) of keystream block blk: the four lanes
+// of a quad compute one block, a column each, the diagonal step by DPP quad
+// permutes.  Every lane of the wave must execute it (the permutes read neighbours).
+__device__ __forceinline__ gk_u128 gk_ks_quad(const GkPad& P, uint32_t blk, uint32_t qi) {
+    const uint32_t a0 = gk_sel4(kChaC0, kChaC1, kChaC2, kChaC3, qi);
+    const uint32_t b0 = gk_sel4(P.k[0], P.k[1], P.k[2], P.k[3], qi);
+    const uint32_t c0 = gk_sel4(P.k[4], P.k[5], P.k[6], P.k[7], qi);
+    const uint32_t d0 = gk_sel4(blk, P.n[0], P.n[1], P.n[2], qi);
+    uint32_t a = a0, b = b0, c = c0, d = d0;
+#pragma unroll
+    for (int r = 0; r < HY_GK_PAD_ROUNDS / 2; ++r) {
+        GK_QR(a, b, c, d);   // column round
+        b = qperm32<kQRot1>(b);
+        c = qperm32<kQRot2>(c);
+        d = qperm32<kQRot3>(d);
+        GK_QR(a, b, c, d);   // diagonal round
+        b = qperm32<kQRot3>(b);
+        c = qperm32<kQRot2>(c);
+        d = qperm32<kQRot1>(d);
+    }
+    return (gk_u128)(d + d0) << 96 | (gk_u128)(c + c0) << 64 | (gk_u128)(b + b0) << 32 | (a + a0);
+}
+
+// The same column computed by one lane alone (edge chunks, divergent code).
+__device__ __forceinline__ gk_u128 gk_ks_single(const GkPad& P, uint32_t blk, uint32_t col) {
+    uint32_t x[16] = {kChaC0, kChaC1, kChaC2, kChaC3, P.k[0], P.k[1], P.k[2], P.k[3],
+                      P.k[4], P.k[5], P.k[6], P.k[7], blk,    P.n[0], P.n[1], P.n[2]};
+    uint32_t s[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) s[i] = x[i];
+#pragma unroll
+    for (int r = 0; r < HY_GK_PAD_ROUNDS / 2; ++r) {
+        GK_QR(x[0], x[4], x[8], x[12]);
+        GK_QR(x[1], x[5], x[9], x[13]);
+        GK_QR(x[2], x[6], x[10], x[14]);
+        GK_QR(x[3], x[7], x[11], x[15]);
+        GK_QR(x[0], x[5], x[10], x[15]);
+        GK_QR(x[1], x[6], x[11], x[12]);
+        GK_QR(x[2], x[7], x[8], x[13]);
+        GK_QR(x[3], x[4], x[9], x[14]);
+    }
+    uint32_t w[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) w[j] = gk_sel4(x[4 * j] + s[4 * j], x[4 * j + 1] + s[4 * j + 1], x[4 * j + 2] + s[4 * j + 2],
+                                               x[4 * j + 3] + s[4 * j + 3], col);
+    return (gk_u128)w[3] << 96 | (gk_u128)w[2] << 64 | (gk_u128)w[1] << 32 | w[0];
+}
+
+// Keystream bytes [W0, W0 + 16) for any W0 (one or two columns).
+__device__ __forceinline__ gk_u128 gk_ks_at(const GkPad& P, uint64_t W0) {
+    const uint64_t c0 = W0 & ~15ull;
+    const uint32_t sh = (uint32_t)(W0 & 15);
+    const gk_u128 x0 = gk_ks_single(P, (uint32_t)(c0 >> 6), (uint32_t)(c0 >> 4) & 3u);
+    if (!sh) return x0;
+    const gk_u128 x1 = gk_ks_single(P, (uint32_t)((c0 + 16) >> 6), (uint32_t)((c0 + 16) >> 4) & 3u);
+    return (x0 >> (8 * sh)) | (x1 << (8 * (16 - sh)));
 }
 
 #ifndef HY_GK_FORCE_WINDOWS
@@ -78,8 +150,8 @@ __device__ __forceinline__ gk_u128 gk_pad_at(uint64_t seed, uint64_t f, int32_t 
 
 // Frame k's bytes in the 16-byte wire chunk at rel (group-relative, 16-aligned)
 // address a: salt, then header / padding / chunk XOR the frame's key.
-__device__ __forceinline__ void gk_contrib(const hyobfs_gecko_batch& B, const GeckoGroup& G, uint64_t f0, uint32_t k,
-                                           uint32_t a, gk_u128& r, uint32_t& cov) {
+__device__ __forceinline__ void gk_contrib(const hyobfs_gecko_batch& B, const GkPad& P, const GeckoGroup& G, uint64_t base,
+                                           uint32_t k, uint32_t a, gk_u128& r, uint32_t& cov) {
     const uint32_t hpl = G.hp_plain[k];
     if (!hpl) return;
     const int32_t hp = (int32_t)(hpl & 0xffff), plain = (int32_t)(hpl >> 16);
@@ -94,7 +166,9 @@ __device__ __forceinline__ void gk_contrib(const hyobfs_gecko_batch& B, const Ge
             X |= (p0 <= 0 ? H << (8 * -p0) : H >> (8 * p0)) & gk_mask(xlo - p0, hhi - p0);
         }
         const int32_t plo = max(p0, (int32_t)HYOBFS_GECKO_HEADER_LEN), phi = min(p0 + 16, hp);
-        if (plo < phi) X |= gk_pad_at(B.pad_seed, f0 + k, p0) & gk_mask(plo - p0, phi - p0);
+        if (plo < phi)   // the 16-aligned wire chunk at base + a is one keystream column
+            X |= gk_ks_single(P, (uint32_t)((base + a) >> 6), (uint32_t)((base + a) >> 4) & 3u) &
+                 gk_mask(plo - p0, phi - p0);
         const int32_t clo = max(p0, hp);
         if (clo < xhi) {   // chunk bytes
             const uint8_t* __restrict__ ch = B.msg + G.chunk_off[k];
@@ -126,7 +200,9 @@ __device__ __forceinline__ void gecko_encode_aligned(const KeyParams& K, const h
                                                   uint64_t prevE, uint64_t maxE, unsigned long long vmask,
                                                   uint32_t plain, uint64_t salt, gk_u128 k0, gk_u128 k1) {
     (void)K;
-    // 256-aligned: each wave store instruction (64 lanes x 16 B) covers whole 128-B lines
+    const GkPad P = gk_pad_params(B);
+    // 256-aligned: each wave store instruction (64 lanes x 16 B) covers whole 128-B lines,
+    // and the quads of a store instruction hold whole 64-byte keystream blocks
     const uint64_t base = uni64(__shfl(oo, (int)__builtin_ctzll(vmask), 64)) & ~255ull;
     const uint32_t rs = valid ? (uint32_t)(oo - base) : (prevE > base ? (uint32_t)(prevE - base) : 0u);
     const uint32_t rend = (uint32_t)(maxE - base);
@@ -178,7 +254,7 @@ __device__ __forceinline__ void gecko_encode_aligned(const KeyParams& K, const h
             if (interior(lane, a, p, php)) continue;
             gk_u128 r = 0;
             uint32_t cov = 0;
-            for (uint32_t k = lane; k < 64 && G.rs[k] < a + 16; ++k) gk_contrib(B, G, f0, k, a, r, cov);
+            for (uint32_t k = lane; k < 64 && G.rs[k] < a + 16; ++k) gk_contrib(B, P, G, base, k, a, r, cov);
             if (cov == 0xFFFFu) gk_store16u(ob + a, r);   // a plain store: the line stays in L2 for the sweep's part
             else if (cov) store_masked(ob + a, r, cov);
         }
@@ -193,15 +269,19 @@ __device__ __forceinline__ void gecko_encode_aligned(const KeyParams& K, const h
             const uint32_t c = T + lane + 64 * u, a = 16 * c;
             v[u] = 0;
             ok[u] = false;
+            bool pad = false;
             if (c < tc) {
                 while (G.rs[q + 1] <= a) ++q;   // rs[64] = the range end > a stops it
                 int32_t p, hp;
                 ok[u] = interior(q, a, p, hp);
-                if (ok[u]) {
-                    v[u] = p >= hp ? gk_load16u(B.msg + G.chunk_off[q] + (p - hp)) : gk_pad_at(B.pad_seed, f0 + q, p);
-                    v[u] ^= G.key[2 * q + ((a >> 4) & 1)];
-                }
+                pad = ok[u] && p < hp;
+                if (ok[u] && !pad) v[u] = gk_load16u(B.msg + G.chunk_off[q] + (p - hp));
             }
+            if (__ballot(pad)) {   // the whole wave: a quad computes one 64-byte block
+                const gk_u128 ks = gk_ks_quad(P, (uint32_t)((base + 16ull * c) >> 6), lane & 3u);
+                if (pad) v[u] = ks;
+            }
+            if (ok[u]) v[u] ^= G.key[2 * q + ((a >> 4) & 1)];
         }
 #pragma unroll
         for (int u = 0; u < kGkU; ++u)
@@ -298,13 +378,12 @@ __global__ __launch_bounds__(256) HY_GK_ATTR void gecko_encode_kernel(KeyParams 
     auto interior = [](uint32_t p, uint32_t hp, uint32_t plain) {
         return (p >= hp && p + 16 <= plain) || (p >= HYOBFS_GECKO_HEADER_LEN && p + 16 <= hp);
     };
-    auto pad16 = [&](uint32_t k, uint32_t p) -> gk_u128 {   // pad stream at plaintext [p, p+16) of frame f0+k
+    const GkPad P = gk_pad_params(B);
+    auto pad16 = [&](uint32_t k, uint32_t p) -> gk_u128 {   // keystream at plaintext [p, p+16) of frame f0+k
 #ifdef HY_X_NOPAD   // ablation builds only (timing experiments; wrong output)
         return (gk_u128)(f0 + k + p);
 #else
-        const uint64_t w = ((f0 + k) * HYOBFS_GECKO_BUFFER_SIZE + p) >> 3;
-        const uint64_t z0 = B.pad_seed + (w + 1) * 0x9e3779b97f4a7c15ull;   // SplitMix64 outputs w and w + 1
-        return (gk_u128)gk_mix64(z0 + 0x9e3779b97f4a7c15ull) << 64 | gk_mix64(z0);
+        return gk_ks_at(P, G.out_off[k] + HYOBFS_SALT_LEN + p);
 #endif
     };
     auto store = [&](uint32_t k, uint32_t p, uint32_t plain, gk_u128 v) {

@@ -2,6 +2,7 @@
 // encodeFrame / decodeFrame (gecko_frame.go:39-86) and randomPadLen
 // (gecko.go:131-138).  Plain host C++; the device batch calls live in
 // gecko.hip and hyobfs_api.cpp.
+#include <errno.h>
 #include <sys/random.h>
 
 #include <algorithm>
@@ -14,6 +15,7 @@ namespace {
 bool fill_random(uint8_t* p, size_t n) {   // crypto/rand.Read
     while (n) {
         const ssize_t r = getrandom(p, n, 0);
+        if (r < 0 && errno == EINTR) continue;
         if (r < 0) return false;
         p += r;
         n -= (size_t)r;
@@ -28,6 +30,11 @@ bool chunks_ok(unsigned total, unsigned idx) {
 }  // namespace
 
 extern "C" {
+
+int hyobfs_gecko_random_pad_key(uint8_t key[32], uint8_t nonce[12]) {   // crypto/rand, gecko_frame.go:55
+    if (!key || !nonce) return HYOBFS_ERR_INVALID;
+    return fill_random(key, 32) && fill_random(nonce, 12) ? HYOBFS_OK : HYOBFS_ERR_IO;
+}
 
 int64_t hyobfs_gecko_encode_frame(const hyobfs_gecko_header* h, const uint8_t* payload, size_t len, uint8_t* out,
                                   size_t cap) {

@@ -225,6 +225,16 @@ __device__ __forceinline__ void store_masked(uint8_t* dst, u128 r, uint32_t cov)
     }
 }
 
+// quad_perm DPP move (lane i of each quad reads lane CTRL[i]): the diagonal steps of
+// four-lanes-per-state BLAKE2b (salamander_tile.h) and ChaCha (gecko.hip)
+template <int CTRL>
+__device__ __forceinline__ uint32_t qperm32(uint32_t x) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, CTRL, 0xF, 0xF, false);
+}
+constexpr int kQRot1 = 0x39;   // quad_perm [1,2,3,0]: lane i reads lane i+1
+constexpr int kQRot2 = 0x4E;   // [2,3,0,1]
+constexpr int kQRot3 = 0x93;   // [3,0,1,2]
+
 // Values that are equal in every lane (read from LDS, reduced) made scalar, so
 // loop bounds and base pointers live in SGPRs and loops stay wave-uniform.
 // (the builtin returns int: convert each half to uint32_t before widening)

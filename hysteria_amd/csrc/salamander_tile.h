@@ -106,13 +106,8 @@ __device__ __forceinline__ uint64_t quad_msg(const KeyParams& K, uint64_t lo, ui
 // quad_perm DPP move of a 64-bit value (lane i of each quad reads lane CTRL[i])
 template <int CTRL>
 __device__ __forceinline__ uint64_t qperm(uint64_t x) {
-    const uint32_t lo = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)x, CTRL, 0xF, 0xF, false);
-    const uint32_t hi = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)(x >> 32), CTRL, 0xF, 0xF, false);
-    return (uint64_t)hi << 32 | lo;
+    return (uint64_t)qperm32<CTRL>((uint32_t)(x >> 32)) << 32 | qperm32<CTRL>((uint32_t)x);
 }
-constexpr int kQRot1 = 0x39;   // quad_perm [1,2,3,0]: lane i reads lane i+1
-constexpr int kQRot2 = 0x4E;   // [2,3,0,1]
-constexpr int kQRot3 = 0x93;   // [3,0,1,2]
 
 #define HY_QG(a, b, c, d, x, y)   \
     do {                          \

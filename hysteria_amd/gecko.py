@@ -77,7 +77,8 @@ class HyobfsGeckoHeader(ctypes.Structure):
 
 class HyobfsGeckoBatch(ctypes.Structure):
     _fields_ = [("n", ctypes.c_uint64), ("msg", ctypes.c_void_p), ("frames", ctypes.c_void_p),
-                ("salts", ctypes.c_void_p), ("pad_seed", ctypes.c_uint64), ("out", ctypes.c_void_p),
+                ("salts", ctypes.c_void_p), ("pad_key", ctypes.c_uint8 * 32), ("pad_nonce", ctypes.c_uint8 * 12),
+                ("reserved_", ctypes.c_uint32), ("out", ctypes.c_void_p),
                 ("out_off", ctypes.c_void_p), ("workspace", ctypes.c_void_p), ("workspace_bytes", ctypes.c_uint64)]
 
 
@@ -100,7 +101,8 @@ def _glib():
                 ("hyobfs_gecko_pad_len", u32, [i32, i32, u32, u32]),
                 ("hyobfs_gecko_workspace_size", u64, [u64]),
                 ("hyobfs_gecko_encode_batch", i32, [vp, ctypes.POINTER(HyobfsGeckoBatch), vp]),
-                ("hyobfs_gecko_parse_batch", i32, [vp, vp, vp, u64, vp, vp])):
+                ("hyobfs_gecko_parse_batch", i32, [vp, vp, vp, u64, vp, vp]),
+                ("hyobfs_gecko_random_pad_key", i32, [vp, vp])):
             f = getattr(lib, name)
             f.restype, f.argtypes = res, args
         lib._gecko_declared = True
@@ -382,11 +384,21 @@ def workspace_size(n: int) -> int:
     return int(_glib().hyobfs_gecko_workspace_size(n))
 
 
-def encode_batch(obfuscator, *, msg, frames, salts, pad_seed: int, out, out_off, workspace=None, n=None,
-                 stream=None) -> None:
+def random_pad_key() -> tuple[bytes, bytes]:
+    """A fresh (key, nonce) for the padding keystream from the OS (hyobfs_gecko_random_pad_key,
+    getrandom: the source of the reference's crypto/rand)."""
+    key, nonce = ctypes.create_string_buffer(32), ctypes.create_string_buffer(12)
+    check(_glib().hyobfs_gecko_random_pad_key(key, nonce), "random_pad_key")
+    return key.raw, nonce.raw
+
+
+def encode_batch(obfuscator, *, msg, frames, salts, out, out_off, pad_key: bytes | None = None,
+                 pad_nonce: bytes | None = None, workspace=None, n=None, stream=None) -> None:
     """hyobfs_gecko_encode_batch: every frame's wire datagram in one device pass.
     Arguments are device tensors (torch) or device pointers; the shipped kernel
-    needs no workspace (workspace_size() == 0)."""
+    needs no workspace (workspace_size() == 0).  Padding is a keyed keystream
+    (include/hyobfs_gecko.h): a fresh OS-random key per call unless pad_key and
+    pad_nonce are given (reproducible output for tests)."""
     from .salamander import _ptr, _stream
     if n is None:   # frames: 16-byte hyobfs_gecko_frame records
         n = frames.numel() * frames.element_size() // FRAME_DTYPE.itemsize if hasattr(frames, "numel") else len(frames)
@@ -394,7 +406,13 @@ def encode_batch(obfuscator, *, msg, frames, salts, pad_seed: int, out, out_off,
         ws_bytes = 0
     else:
         ws_bytes = workspace.numel() * workspace.element_size() if hasattr(workspace, "numel") else workspace_size(n)
-    b = HyobfsGeckoBatch(n=n, msg=_ptr(msg), frames=_ptr(frames), salts=_ptr(salts), pad_seed=pad_seed,
+    if pad_key is None or pad_nonce is None:
+        pad_key, pad_nonce = random_pad_key()
+    if len(pad_key) != 32 or len(pad_nonce) != 12:
+        raise ValueError("pad_key must be 32 bytes and pad_nonce 12")
+    b = HyobfsGeckoBatch(n=n, msg=_ptr(msg), frames=_ptr(frames), salts=_ptr(salts),
+                         pad_key=(ctypes.c_uint8 * 32).from_buffer_copy(pad_key),
+                         pad_nonce=(ctypes.c_uint8 * 12).from_buffer_copy(pad_nonce),
                          out=_ptr(out), out_off=_ptr(out_off), workspace=_ptr(workspace), workspace_bytes=ws_bytes)
     check(_glib().hyobfs_gecko_encode_batch(obfuscator._h, ctypes.byref(b), _stream(stream, out)), "gecko_encode_batch")
 

@@ -95,9 +95,18 @@ typedef struct hyobfs_gecko_batch {
     const uint8_t* msg;                  /* message bytes (device) */
     const hyobfs_gecko_frame* frames;    /* n frames (device) */
     const uint64_t* salts;               /* n Salamander salts (device), as hyobfs_batch.salts */
-    uint64_t pad_seed;                   /* pad byte j of frame i = byte i*2048 + 5 + j (its
-                                            plaintext position) of the little-endian
-                                            SplitMix64(pad_seed) stream */
+    /* Padding (the reference fills it from crypto/rand, gecko_frame.go:55): a keyed
+       keystream, ChaCha with 8 rounds (the RFC 8439 block: constants, pad_key as
+       8 little-endian words, a 32-bit block counter, pad_nonce as 3 words), each
+       64-byte block's bytes in column order (bytes 16c..16c+15 = state words c,
+       c+4, c+8, c+12 after the final addition).  Pad byte j of frame i is
+       keystream byte out_off[i] + 13 + j: its offset in `out`, so every pad byte
+       of a batch takes a different keystream byte (out must stay below 256 GiB).
+       Draw a fresh key per batch (hyobfs_gecko_random_pad_key, getrandom); an
+       explicit key makes the output reproducible (tests, oracle/gecko_ref.py). */
+    uint8_t pad_key[32];
+    uint8_t pad_nonce[12];
+    uint32_t reserved_;
     uint8_t* out;                        /* device */
     const uint64_t* out_off;             /* frame i's wire datagram at out + out_off[i] (device);
                                             its length is 8 + 5 + pad_len + chunk_len */
@@ -108,6 +117,9 @@ typedef struct hyobfs_gecko_batch {
 } hyobfs_gecko_batch;
 
 uint64_t hyobfs_gecko_workspace_size(uint64_t n);
+/* A fresh 256-bit pad key and 96-bit nonce from the OS (getrandom, the source of
+   crypto/rand).  Returns HYOBFS_OK or HYOBFS_ERR_IO. */
+int hyobfs_gecko_random_pad_key(uint8_t key[32], uint8_t nonce[12]);
 /*
  * Encode and obfuscate every frame in one pass on the context's device:
  * out = salt || (header || pad || chunk) ^ BLAKE2b-256(PSK || salt)[i % 32]

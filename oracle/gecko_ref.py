@@ -14,15 +14,18 @@ Restated from the reference (paths relative to apernet/hysteria):
 * ``extras/obfs/gecko.go:170-193``      -- ``ReadFrom``: ``n <= 0`` skipped, top bit clear passed through
 
 Randomness (crypto/rand in the reference) is an explicit input here: pad bytes
-come from the SplitMix64 stream of ``include/hyobfs_gecko.h`` (byte ``i*2048+5+j``
-of stream ``pad_seed`` for pad byte *j* of frame *i*), so device output is
-deterministic and comparable byte for byte.  The reference's own tests
+come from the keyed keystream of ``include/hyobfs_gecko.h`` -- ChaCha with 8
+rounds (RFC 8439 block layout), block bytes in column order, pad byte *j* of frame
+*i* = keystream byte ``out_off[i] + 13 + j`` -- so with an explicit key the device
+output is deterministic and comparable byte for byte.  The block function is
+pinned to RFC 8439 section 2.3.2 at 20 rounds (``tests/test_gecko.py``).  The reference's own tests
 (``gecko_frame_test.go``, ``gecko_test.go``) check round trips, header fields,
 error kinds and size bands, not wire bytes; the same properties are what this
 restatement is tested against (``tests/test_gecko.py``).
 """
 from __future__ import annotations
 
+import struct
 from dataclasses import dataclass
 
 from . import salamander_ref as sref
@@ -93,19 +96,59 @@ def split_chunks(msg_len: int, chunks: int) -> list[tuple[int, int]]:
     return [(i * size, msg_len if i == chunks - 1 else (i + 1) * size) for i in range(chunks)]
 
 
-def pad_bytes(pad_seed: int, frame: int, n: int) -> bytes:
-    """Pad bytes of frame i: bytes i*2048 + 5 + j (plaintext positions) of the stream."""
-    return sref.stream_bytes(pad_seed, frame * BUFFER_SIZE + HEADER_LEN, n)
+CHACHA_C = (0x61707865, 0x3320646E, 0x79622D32, 0x6B206574)
+PAD_ROUNDS = 8
 
 
-def encode_wire(psk: bytes, msg: bytes, frames, salts, pad_seed: int) -> list[bytes]:
+def _rotl(x, n):
+    return ((x << n) | (x >> (32 - n))) & 0xFFFFFFFF
+
+
+def chacha_block(key: bytes, counter: int, nonce: bytes, rounds: int = PAD_ROUNDS) -> list[int]:
+    """RFC 8439 2.3 block function with ``rounds`` rounds: the 16 output words."""
+    s = list(CHACHA_C) + list(struct.unpack("<8I", key)) + [counter & 0xFFFFFFFF] + list(struct.unpack("<3I", nonce))
+    x = list(s)
+
+    def qr(a, b, c, d):
+        x[a] = (x[a] + x[b]) & 0xFFFFFFFF; x[d] = _rotl(x[d] ^ x[a], 16)
+        x[c] = (x[c] + x[d]) & 0xFFFFFFFF; x[b] = _rotl(x[b] ^ x[c], 12)
+        x[a] = (x[a] + x[b]) & 0xFFFFFFFF; x[d] = _rotl(x[d] ^ x[a], 8)
+        x[c] = (x[c] + x[d]) & 0xFFFFFFFF; x[b] = _rotl(x[b] ^ x[c], 7)
+    for _ in range(rounds // 2):
+        qr(0, 4, 8, 12); qr(1, 5, 9, 13); qr(2, 6, 10, 14); qr(3, 7, 11, 15)
+        qr(0, 5, 10, 15); qr(1, 6, 11, 12); qr(2, 7, 8, 13); qr(3, 4, 9, 14)
+    return [(a + b) & 0xFFFFFFFF for a, b in zip(x, s)]
+
+
+def keystream(key: bytes, nonce: bytes, start: int, n: int) -> bytes:
+    """Pad keystream bytes [start, start + n): block b's bytes 16c..16c+15 are its
+    words c, c+4, c+8, c+12 (column order, include/hyobfs_gecko.h)."""
+    out = bytearray()
+    pos = start
+    while len(out) < n:
+        blk = pos // 64
+        w = chacha_block(key, blk, nonce)
+        col = b"".join(struct.pack("<4I", w[c], w[c + 4], w[c + 8], w[c + 12]) for c in range(4))
+        take = min(64 - pos % 64, n - len(out))
+        out += col[pos % 64:pos % 64 + take]
+        pos += take
+    return bytes(out)
+
+
+def pad_bytes(key: bytes, nonce: bytes, wire_off: int, n: int) -> bytes:
+    """Pad bytes of the frame whose wire datagram starts at out offset wire_off."""
+    return keystream(key, nonce, wire_off + 8 + HEADER_LEN, n)
+
+
+def encode_wire(psk: bytes, msg: bytes, frames, salts, pad_key: bytes, pad_nonce: bytes, out_off) -> list[bytes]:
     """Wire datagrams of a frame batch: Salamander(encodeFrame(...)).
 
-    frames: iterable of (chunk_off, chunk_len, pad_len, msg_id, idx_total)."""
+    frames: iterable of (chunk_off, chunk_len, pad_len, msg_id, idx_total);
+    out_off[i]: frame i's offset in the output (it selects its pad keystream)."""
     out = []
     for i, (off, clen, plen, mid, it) in enumerate(frames):
         h = Header(pad_len=plen, msg_id=mid, chunk_idx=it >> 4, total_chunks=it & 0x0F)
-        plain = encode_frame(h, msg[off:off + clen], pad_bytes(pad_seed, i, plen))
+        plain = encode_frame(h, msg[off:off + clen], pad_bytes(pad_key, pad_nonce, int(out_off[i]), plen))
         out.append(sref.obfuscate(psk, plain, int(salts[i]).to_bytes(8, "little")))
     return out
 

@@ -41,6 +41,7 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline (counter passes)")
     args = ap.parse_args()
     import torch
     from hysteria_amd import quic
@@ -89,7 +90,7 @@ def main():
     host = src.cpu().numpy()
     co = ref.CQuicOracle()
     cpu = {}
-    for th in (1, args.cpu_threads):
+    for th in (() if args.no_cpu else (1, args.cpu_threads)):
         m = min(n, 4096 * th)
         t0 = time.perf_counter()
         reps = 0
@@ -106,10 +107,11 @@ def main():
         "value": round(n / (ms / 1e3)), "unit": "packets/s", "n_packets": n, "steps": args.steps,
         "ms_per_batch": round(ms, 4), "packet_GBs": round(byts / (ms / 1e3) / 1e9, 2),
         "restore_copy_ms": round(copy_ms / args.steps, 4),
-        "cpu_baseline": {"value": round(cpu[args.cpu_threads][0]), "unit": "packets/s", "cores": args.cpu_threads,
-                         "kind": "port", "single_thread_value": round(cpu[1][0]),
-                         "sample": f"{cpu[args.cpu_threads][1]} packets on {args.cpu_threads} threads + {cpu[1][1]} on 1 "
-                                   "through oracle/quic_ref.c (AES T-tables, 4-bit GHASH), ~5 s each"}}))
+        "cpu_baseline": None if args.no_cpu else {
+            "value": round(cpu[args.cpu_threads][0]), "unit": "packets/s", "cores": args.cpu_threads,
+            "kind": "port", "single_thread_value": round(cpu[1][0]),
+            "sample": f"{cpu[args.cpu_threads][1]} packets on {args.cpu_threads} threads + {cpu[1][1]} on 1 "
+                      "through oracle/quic_ref.c (AES T-tables, 4-bit GHASH), ~5 s each"}}))
 
 
 if __name__ == "__main__":

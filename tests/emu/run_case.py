@@ -188,9 +188,10 @@ def case_gecko(n_msgs, seed, layout=0):
     ws = np.zeros(gecko.workspace_size(nf), np.uint8)
     o = SalamanderObfuscator(psk, 0)
     p = lambda a: a.ctypes.data  # noqa: E731
-    gecko.encode_batch(o, msg=p(msg), frames=p(fr), salts=p(salts), pad_seed=99, out=p(out), out_off=p(off),
-                       workspace=p(ws), n=nf, stream=0)
-    exp = gref.encode_wire(psk, msg.tobytes(), fr.tolist(), salts, 99)
+    key, nonce = bytes(range(3, 35)), bytes(range(40, 52))
+    gecko.encode_batch(o, msg=p(msg), frames=p(fr), salts=p(salts), pad_key=key, pad_nonce=nonce, out=p(out),
+                       out_off=p(off), workspace=p(ws), n=nf, stream=0)
+    exp = gref.encode_wire(psk, msg.tobytes(), fr.tolist(), salts, key, nonce, off)
     assert out[total:].tobytes() == b"\xa5" * 64
     written = np.zeros(total + 64, bool)
     for i in range(nf):

@@ -418,3 +418,21 @@ def test_plan_fragments_covers_messages_in_band():
     assert i == len(fr)
     widths = 13 + fr["chunk_len"].astype(np.uint64) + fr["pad_len"]
     assert np.array_equal(off[1:], np.cumsum(widths)[:-1]) and total == int(widths.sum())
+
+
+def test_pad_keystream_block_pinned_to_rfc8439():
+    """The Gecko padding keystream (include/hyobfs_gecko.h) is the RFC 8439 ChaCha
+    block with 8 rounds and column-ordered bytes.  At 20 rounds the same block
+    function gives RFC 8439 2.3.2's test vector (row order), so only the round
+    count and the byte order differ from the published function."""
+    import struct
+    from oracle import gecko_ref as gref
+    key, nonce = bytes(range(32)), bytes.fromhex("000000090000004a00000000")
+    w = gref.chacha_block(key, 1, nonce, rounds=20)
+    assert struct.pack("<16I", *w).hex() == (
+        "10f1e7e4d13b5915500fdd1fa32071c4c7d1f4c733c068030422aa9ac3d46c4e"
+        "d2826446079faa0914c2d705d98b02a2b5129cd1de164eb9cbd083e8a2503c4e")
+    w8 = gref.chacha_block(key, 1, nonce)
+    col = b"".join(struct.pack("<4I", w8[c], w8[c + 4], w8[c + 8], w8[c + 12]) for c in range(4))
+    assert gref.keystream(key, nonce, 64, 64) == col
+    assert gref.keystream(key, nonce, 70, 20) == col[6:26]

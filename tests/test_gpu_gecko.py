@@ -13,6 +13,7 @@ from oracle import salamander_ref as sref
 
 pytestmark = pytest.mark.gpu
 PSK = b"average_password"
+KEY, NONCE = bytes(range(7, 39)), bytes(range(100, 112))   # explicit pad keystream key: reproducible wire
 
 
 def _dev(a, gpu):
@@ -41,12 +42,12 @@ def test_encode_batch_vs_oracle(gpu, n_msgs, lo, hi):
     try:
         out = torch.full((total + 64,), 0xA5, dtype=torch.uint8, device=gpu)
         ws = torch.empty(gecko.workspace_size(nf), dtype=torch.uint8, device=gpu)
-        gecko.encode_batch(o, msg=_dev(msg, gpu), frames=_dev(fr, gpu), salts=_dev(salts, gpu), pad_seed=1234,
+        gecko.encode_batch(o, msg=_dev(msg, gpu), frames=_dev(fr, gpu), salts=_dev(salts, gpu), pad_key=KEY, pad_nonce=NONCE,
                            out=out, out_off=_dev(off, gpu), workspace=ws, n=nf)
         got = out.cpu().numpy()
     finally:
         o.close()
-    exp = gref.encode_wire(PSK, msg.tobytes(), fr.tolist(), salts, 1234)
+    exp = gref.encode_wire(PSK, msg.tobytes(), fr.tolist(), salts, KEY, NONCE, off)
     assert got[total:].tobytes() == b"\xa5" * 64
     for i in range(nf):
         assert got[int(off[i]):int(off[i]) + len(exp[i])].tobytes() == exp[i], i
@@ -72,12 +73,12 @@ def test_encode_batch_psk_lengths(gpu, psk_len):
     try:
         out = torch.zeros((total,), dtype=torch.uint8, device=gpu)
         ws = torch.empty(gecko.workspace_size(nf), dtype=torch.uint8, device=gpu)
-        gecko.encode_batch(o, msg=_dev(msg, gpu), frames=_dev(fr, gpu), salts=_dev(salts, gpu), pad_seed=psk_len,
+        gecko.encode_batch(o, msg=_dev(msg, gpu), frames=_dev(fr, gpu), salts=_dev(salts, gpu), pad_key=KEY, pad_nonce=NONCE,
                            out=out, out_off=_dev(off, gpu), workspace=ws, n=nf)
         got = out.cpu().numpy()
     finally:
         o.close()
-    exp = gref.encode_wire(psk, msg.tobytes(), fr.tolist(), salts, psk_len)
+    exp = gref.encode_wire(psk, msg.tobytes(), fr.tolist(), salts, KEY, NONCE, off)
     for i in range(nf):
         assert got[int(off[i]):int(off[i]) + len(exp[i])].tobytes() == exp[i], i
 
@@ -95,16 +96,16 @@ def test_encode_batch_skips_impossible_frames(gpu):
     try:
         out = torch.full((2100 * len(fr),), 0xA5, dtype=torch.uint8, device=gpu)
         ws = torch.empty(gecko.workspace_size(len(fr)), dtype=torch.uint8, device=gpu)
-        gecko.encode_batch(o, msg=_dev(msg, gpu), frames=_dev(fr, gpu), salts=_dev(salts, gpu), pad_seed=5,
+        gecko.encode_batch(o, msg=_dev(msg, gpu), frames=_dev(fr, gpu), salts=_dev(salts, gpu), pad_key=KEY, pad_nonce=NONCE,
                            out=out, out_off=_dev(off, gpu), workspace=ws)
         got = out.cpu().numpy()
     finally:
         o.close()
-    exp = gref.encode_wire(PSK, msg.tobytes(), fr.tolist()[:1], salts[:1], 5)[0]
+    exp = gref.encode_wire(PSK, msg.tobytes(), fr.tolist()[:1], salts[:1], KEY, NONCE, off[:1])[0]
     assert got[:len(exp)].tobytes() == exp
     for i in (1, 2, 3):   # one chunk, index >= total, datagram over 2048 bytes: untouched
         assert (got[2100 * i:2100 * (i + 1)] == 0xA5).all(), i
-    plain4 = gref.encode_frame(gref.Header(3, 2, 1, 2), msg[10:20].tobytes(), gref.pad_bytes(5, 4, 3))
+    plain4 = gref.encode_frame(gref.Header(3, 2, 1, 2), msg[10:20].tobytes(), gref.pad_bytes(KEY, NONCE, 4 * 2100, 3))
     exp4 = sref.obfuscate(PSK, plain4, int(salts[4]).to_bytes(8, "little"))
     assert got[4 * 2100:4 * 2100 + len(exp4)].tobytes() == exp4
 
@@ -124,7 +125,7 @@ def test_parse_batch_and_reassembly(gpu):
         wire = torch.empty(total + 16, dtype=torch.uint8, device=gpu)
         ws = torch.empty(gecko.workspace_size(nf), dtype=torch.uint8, device=gpu)
         d_off = _dev(off, gpu)
-        gecko.encode_batch(o, msg=_dev(msg, gpu), frames=_dev(fr, gpu), salts=_dev(salts, gpu), pad_seed=77,
+        gecko.encode_batch(o, msg=_dev(msg, gpu), frames=_dev(fr, gpu), salts=_dev(salts, gpu), pad_key=KEY, pad_nonce=NONCE,
                            out=wire, out_off=d_off, workspace=ws, n=nf)
         wl = (13 + fr["chunk_len"].astype(np.uint32) + fr["pad_len"]).astype(np.uint32)
         # append a short-header datagram, a dropped (8-byte) one and a malformed fragment
@@ -225,13 +226,13 @@ def test_encode_kernel_frame_grid(gpu):
     o = hysteria_amd.SalamanderObfuscator(PSK, 0)
     try:
         out = torch.full((total + 64,), 0xA5, dtype=torch.uint8, device=gpu)
-        gecko.encode_batch(o, msg=_dev(msg, gpu), frames=_dev(fr, gpu), salts=_dev(salts, gpu), pad_seed=99,
+        gecko.encode_batch(o, msg=_dev(msg, gpu), frames=_dev(fr, gpu), salts=_dev(salts, gpu), pad_key=KEY, pad_nonce=NONCE,
                            out=out, out_off=_dev(off, gpu), n=len(fr))
         got = out.cpu().numpy()
     finally:
         o.close()
     assert got[total:].tobytes() == b"\xa5" * 64
-    exp = gref.encode_wire(PSK, msg.tobytes(), fr.tolist(), salts, 99)
+    exp = gref.encode_wire(PSK, msg.tobytes(), fr.tolist(), salts, KEY, NONCE, off)
     for k, (t, i, pad) in enumerate(grid):
         wire = got[int(off[k]):int(off[k]) + int(wl[k])].tobytes()
         assert wire == exp[k], (t, i, pad)
@@ -274,3 +275,46 @@ def test_parse_kernel_decode_frame_rejects(gpu):
     for k, (name, d, want) in enumerate(DECODE_REJECTS):
         assert int(pr[k]["status"]) == getattr(gecko, want), name
         assert int(pr[k]["status"]) == oracle_status[gref.parse(d)[0]], name
+
+
+def test_encode_random_pad_key_padding_is_keystream(gpu):
+    """Default encode_batch draws a fresh OS-random pad key per call (the reference
+    pads from crypto/rand, gecko_frame.go:55): two calls give different padding and
+    the same frames.  Salamander's key repeats every 32 bytes, so the wire exposes
+    pad[j] ^ pad[j+32]; for a keystream pad those bytes are uniform (chi-square over
+    256 bins), unlike a structured generator's."""
+    import torch
+    import hysteria_amd
+    from hysteria_amd import gecko
+    lens, msg = _messages(400, 77)
+    fr, off, total = gecko.plan_fragments(lens, 1100, 1200, first_msg_id=1)
+    nf = len(fr)
+    salts = sref.splitmix64_array(8, 0, nf)
+    o = hysteria_amd.SalamanderObfuscator(PSK, 0)
+    try:
+        outs = []
+        for _ in range(2):
+            out = torch.zeros((total,), dtype=torch.uint8, device=gpu)
+            gecko.encode_batch(o, msg=_dev(msg, gpu), frames=_dev(fr, gpu), salts=_dev(salts, gpu), out=out,
+                               out_off=_dev(off, gpu), n=nf)
+            outs.append(out.cpu().numpy())
+    finally:
+        o.close()
+    diffs, same_frames = [], 0
+    for i in range(nf):
+        plen = int(fr[i]["pad_len"])
+        w = [x[int(off[i]):int(off[i]) + 13 + plen + int(fr[i]["chunk_len"])].tobytes() for x in outs]
+        p = [sref.deobfuscate(PSK, x) for x in w]
+        h0, b0 = gref.decode_frame(p[0])
+        h1, b1 = gref.decode_frame(p[1])
+        assert (h0, b0) == (h1, b1)   # same frames ...
+        same_frames += p[0][5:5 + plen] == p[1][5:5 + plen] and plen > 0
+        if plen > 32:                 # ... what the wire exposes of the padding
+            wire = np.frombuffer(w[0], np.uint8)
+            diffs.append(wire[13:13 + plen - 32] ^ wire[13 + 32:13 + plen])
+    assert same_frames == 0          # ... different padding
+    d = np.concatenate(diffs)
+    counts = np.bincount(d, minlength=256)
+    exp = d.size / 256
+    chi2 = float(((counts - exp) ** 2 / exp).sum())
+    assert d.size > 100_000 and chi2 < 400, (d.size, chi2)   # 255 dof: mean 255, sd ~22.6
