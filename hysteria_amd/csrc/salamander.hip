@@ -13,7 +13,7 @@
 //     One-shot workgroups of 16 datagrams: a key wave beside three data waves.
 //   * salamander_wave_kernel (salamander_wave.h): every other layout (packed
 //     output, ragged lengths, any alignment).  One wave per 64-datagram group.
-#include "salamander_tile.h"
+#include "salamander_ptile.h"
 
 namespace hyobfs {
 
@@ -26,7 +26,9 @@ namespace hyobfs {
     extern template void launch_tile_sw<true, n>(const BatchParams&, const KeyParams&, const TileParams&,   \
                                                  hipStream_t);                                              \
     extern template void launch_tile_sw<false, n>(const BatchParams&, const KeyParams&, const TileParams&,  \
-                                                  hipStream_t);
+                                                  hipStream_t);                                              \
+    extern template void launch_ptile_sw<true, n>(const BatchParams&, const KeyParams&, hipStream_t);       \
+    extern template void launch_ptile_sw<false, n>(const BatchParams&, const KeyParams&, hipStream_t);
 HY_EXTERN_SW(0) HY_EXTERN_SW(1) HY_EXTERN_SW(2) HY_EXTERN_SW(3) HY_EXTERN_SW(4) HY_EXTERN_SW(5)
 HY_EXTERN_SW(6) HY_EXTERN_SW(7) HY_EXTERN_SW(8) HY_EXTERN_SW(9) HY_EXTERN_SW(10) HY_EXTERN_SW(11)
 HY_EXTERN_SW(12) HY_EXTERN_SW(13) HY_EXTERN_SW(14) HY_EXTERN_SW(15)
@@ -169,6 +171,17 @@ static void launch_main(const BatchParams& bp, const KeyParams& k, hipStream_t s
         switch (k.salt_pos >> 3) {
 #define HY_CASE(n) \
     case n: launch_tile_sw<OBF, n>(bp, k, T, s); break;
+            HY_CASE(0) HY_CASE(1) HY_CASE(2) HY_CASE(3) HY_CASE(4) HY_CASE(5) HY_CASE(6) HY_CASE(7)
+            HY_CASE(8) HY_CASE(9) HY_CASE(10) HY_CASE(11) HY_CASE(12) HY_CASE(13) HY_CASE(14)
+            HY_CASE(15)
+#undef HY_CASE
+        }
+        return;
+    }
+    if (PACKED && kc != kKernelWave) {   // every packed batch: the packed tile kernel
+        switch (k.salt_pos >> 3) {
+#define HY_CASE(n) \
+    case n: launch_ptile_sw<OBF, n>(bp, k, s); break;
             HY_CASE(0) HY_CASE(1) HY_CASE(2) HY_CASE(3) HY_CASE(4) HY_CASE(5) HY_CASE(6) HY_CASE(7)
             HY_CASE(8) HY_CASE(9) HY_CASE(10) HY_CASE(11) HY_CASE(12) HY_CASE(13) HY_CASE(14)
             HY_CASE(15)

@@ -7,6 +7,8 @@ streaming kernel by up to +-5 % between processes, is shared.
       python scripts/ab_variants.py [kernels=tile] [L=1200] [P=1048576]
 
 A name ending in "!" is an ablation build (wrong output): its wire is not checked.
+AB_WORKLOAD=bimodal runs BASELINE configs[2] instead (P datagrams of the 40 % 64 B /
+60 % 1350 B mix, default 4M, packed output).
 """
 import os
 import statistics
@@ -24,13 +26,36 @@ K = int(os.environ.get("AB_STEPS", "10"))
 R = int(os.environ.get("AB_ROUNDS", "6"))
 libs = [kv.split("=", 1) for kv in os.environ.get("AB_LIBS", "main=" + hysteria_amd._lib.LIB_PATH).split(",")]
 dev = torch.device("cuda:0")
-inp = torch.empty(P * L, dtype=torch.uint8, device=dev)
-hysteria_amd.synth_stream(inp, P * L, 1, 0)
-salts = torch.empty(P, dtype=torch.int64, device=dev)
-hysteria_amd.synth_u64(salts, P, 2, 0)
-wire = torch.empty(P * (L + 8), dtype=torch.uint8, device=dev)
-back = torch.empty(P * L, dtype=torch.uint8, device=dev)
-obf_bytes, deobf_bytes = P * (2 * L + 16), P * (2 * L + 8)
+WL = os.environ.get("AB_WORKLOAD", "uniform")
+salts = None
+if WL == "bimodal":
+    P = int(sys.argv[3]) if len(sys.argv) > 3 else 1 << 22
+    lens = torch.empty(P, dtype=torch.int32, device=dev)
+    hysteria_amd.synth_bimodal_lengths(lens, P, 3, 0)
+    in_off = torch.zeros(P, dtype=torch.int64, device=dev)
+    in_off[1:] = torch.cumsum(lens[:-1].to(torch.int64), 0)
+    total_in = int(lens.to(torch.int64).sum())
+    inp = torch.empty(total_in + 16, dtype=torch.uint8, device=dev)
+    hysteria_amd.synth_stream(inp, total_in, 1, 0)
+    salts = torch.empty(P, dtype=torch.int64, device=dev)
+    hysteria_amd.synth_u64(salts, P, 2, 0)
+    cap = total_in + 8 * P
+    wire = torch.empty(cap, dtype=torch.uint8, device=dev)
+    out_off = torch.empty(P, dtype=torch.int64, device=dev)
+    out_len = torch.empty(P, dtype=torch.int32, device=dev)
+    back = torch.empty(total_in + 16, dtype=torch.uint8, device=dev)
+    ws = torch.empty(hysteria_amd.workspace_size(P), dtype=torch.uint8, device=dev)
+    obf_bytes, deobf_bytes = 2 * total_in + 16 * P, 2 * total_in + 8 * P
+    PL = total_in
+else:
+    inp = torch.empty(P * L, dtype=torch.uint8, device=dev)
+    hysteria_amd.synth_stream(inp, P * L, 1, 0)
+    salts = torch.empty(P, dtype=torch.int64, device=dev)
+    hysteria_amd.synth_u64(salts, P, 2, 0)
+    wire = torch.empty(P * (L + 8), dtype=torch.uint8, device=dev)
+    back = torch.empty(P * L, dtype=torch.uint8, device=dev)
+    obf_bytes, deobf_bytes = P * (2 * L + 16), P * (2 * L + 8)
+    PL = P * L
 ctxs = {}
 for name, path in libs:
     for k in kernels:
@@ -40,10 +65,16 @@ for name, path in libs:
 
 
 def ob(o):
+    if WL == "bimodal":
+        return lambda: o.obfuscate_batch(inp, P, in_off=in_off, in_len=lens, salts=salts, out=wire, out_cap=cap,
+                                         out_off=out_off, out_len=out_len, workspace=ws, workspace_bytes=ws.numel())
     return lambda: o.obfuscate_batch(inp, P, in_stride=L, len_uniform=L, salts=salts, out=wire, out_stride=L + 8)
 
 
 def de(o):
+    if WL == "bimodal":
+        return lambda: o.deobfuscate_batch(wire, P, in_off=out_off, in_len=out_len, out=back, out_cap=total_in,
+                                           workspace=ws, workspace_bytes=ws.numel())
     return lambda: o.deobfuscate_batch(wire, P, in_stride=L + 8, len_uniform=L + 8, out=back, out_stride=L)
 
 
@@ -54,12 +85,12 @@ for name, (o, nocheck) in ctxs.items():   # every checked variant's output must 
     ob(o)()
     de(o)()
     torch.cuda.synchronize()
-    assert torch.equal(back, inp), f"{name}: round trip"
+    assert torch.equal(back[:PL], inp[:PL]), f"{name}: round trip"
     h = wire[: 1 << 26].clone()
     if ref is None:
         ref = h
     assert torch.equal(h, ref), f"{name}: wire differs"
-cases = [("copy", "obf", lambda: wire[:P * L].copy_(inp), 2 * P * L)]
+cases = [("copy", "obf", lambda: wire[:PL].copy_(inp[:PL]), 2 * PL)]
 for name, (o, _) in ctxs.items():
     cases += [(name, "obf", ob(o), obf_bytes), (name, "deobf", de(o), deobf_bytes)]
 res = {(k, d): [] for k, d, _, _ in cases}
@@ -75,7 +106,7 @@ for r in range(R + 1):
         torch.cuda.synchronize()
         if r:
             res[(k, d)].append(e0.elapsed_time(e1) / K)
-print(f"P={P} L={L} steps={K} rounds={R}")
+print(f"workload={WL} P={P} L={L if WL != 'bimodal' else 'bimodal'} steps={K} rounds={R}")
 for k, d, _, nbytes in cases:
     v = res[(k, d)]
     med = statistics.median(v)

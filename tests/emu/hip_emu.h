@@ -27,6 +27,8 @@
 #include <thread>
 #include <vector>
 
+#include <sanitizer/asan_interface.h>
+
 #define __global__
 #define __device__
 #define __host__
@@ -192,6 +194,7 @@ inline unsigned long long atomicAdd(unsigned long long* p, unsigned long long v)
 
 #define hipLaunchKernelGGL(kernel, grid, block, shmem, stream, ...) \
     hyemu::launch(dim3(grid), dim3(block), (size_t)(shmem), [&] { kernel(__VA_ARGS__); })
+inline bool hyemu_readable(const void* p) { return !__asan_address_is_poisoned(p); }
 inline uint8_t* hyemu_dyn_lds() { return hyemu::g_ctx.dyn.get(); }
 
 // ---- runtime API subset

@@ -62,6 +62,28 @@ def case_ragged(seed, n, maxlen, obf, layout, psk=b"average_password"):
     run(obf, psk, lens, in_off, inp, salts, cap, out_stride=stride)
 
 
+def case_packed_cap(seed, n, maxlen, obf, cap_pct, psk_len):
+    """Packed output with out_cap cut to cap_pct % of the full size (the regions past
+    it, and every later one, dropped), in_off with gaps, a PSK of psk_len bytes; for
+    deobfuscate the input is real wire bytes."""
+    rng = np.random.default_rng(seed)
+    psk = bytes((5 * i + 3) & 0xFF for i in range(psk_len))
+    lens = rng.integers(0, maxlen, n).astype(np.uint32)
+    gaps = rng.integers(0, 5, n)
+    in_off = np.zeros(n, np.uint64)
+    in_off[0] = 3
+    in_off[1:] = 3 + np.cumsum((lens + gaps)[:-1], dtype=np.uint64)
+    inp = rng.integers(0, 256, int(in_off[-1] + lens[-1] + 32), dtype=np.uint8)
+    salts = ref.splitmix64_array(2, 0, n)
+    if not obf:
+        co = ref.COracle()
+        cap = int(lens.sum()) + 8 * n
+        wire, woff, wlen, _ = co.batch(True, psk, n, inp, in_off=in_off, in_len=lens, salts=salts, out_cap=cap)
+        inp, in_off, lens = wire, woff, wlen
+    full = int(lens.sum()) + (8 * n if obf else 0)
+    run(obf, psk, lens, in_off, inp, salts, max(16, full * cap_pct // 100))
+
+
 def case_bimodal(n, obf):
     lens = ref.bimodal_lengths(3, 0, n)
     in_off = np.zeros(n, np.uint64)
@@ -279,6 +301,8 @@ if __name__ == "__main__":
     args = [int(a) for a in sys.argv[2:]]
     if which == "bimodal":
         case_bimodal(args[0], bool(args[1]))
+    elif which == "pcap":
+        case_packed_cap(*args[:3], bool(args[3]), args[4], args[5])
     elif which == "slotted":
         case_slotted(args[0], args[1], bool(args[2]), args[3], args[4], args[5])
     elif which == "uniform":
