@@ -35,17 +35,24 @@ HY_EXTERN_SW(12) HY_EXTERN_SW(13) HY_EXTERN_SW(14) HY_EXTERN_SW(15)
 #undef HY_EXTERN_SW
 
 // ------------------------------------------------------ packed-layout scan
-// Tile sums of the output widths; the main kernel adds a wavefront scan.
+// Tile sums of the output widths (256-datagram scan tiles), and for each
+// 16-datagram tile of the packed tile kernel its offset inside its scan tile.
 template <bool OBF>
 __global__ __launch_bounds__(kTile) void tile_sums_kernel(BatchParams B) {
     __shared__ uint64_t s_w[kTile / 64];
-    const uint64_t p = (uint64_t)blockIdx.x * kTile + threadIdx.x;
+    const uint32_t t = threadIdx.x, lane = t & 63;
+    const uint64_t p = (uint64_t)blockIdx.x * kTile + t;
     uint32_t W = 0;
     if (p < B.n) W = out_width<OBF>(pkt_len(B, p), B.pkt_cap);
-    const uint64_t ws = wave_sum(W);
-    if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = ws;
+    const uint64_t inc = wave_incl_scan((uint64_t)W, (int)lane);
+    if (lane == 63) s_w[t >> 6] = inc;
     __syncthreads();
-    if (threadIdx.x == 0) {
+    if ((t & (kTileMaxD - 1)) == 0 && p < B.n) {
+        uint64_t pre = inc - W;
+        for (uint32_t w = 0; w < (t >> 6); ++w) pre += s_w[w];
+        B.sub_prefix[p / kTileMaxD] = pre;
+    }
+    if (t == 0) {
         uint64_t s = 0;
 #pragma unroll
         for (int i = 0; i < kTile / 64; ++i) s += s_w[i];
@@ -207,6 +214,7 @@ hipError_t launch_salamander(bool obf, const BatchParams& b, const KeyParams& k,
     BatchParams bp = b;
     if (b.out_stride == 0) {
         const dim3 grid((uint32_t)ntiles), block(kTile);
+        bp.sub_prefix = bp.tile_sums + ntiles + 1;   // hyobfs_batch_workspace_size
         if (obf)
             hipLaunchKernelGGL(tile_sums_kernel<true>, grid, block, 0, s, bp);
         else

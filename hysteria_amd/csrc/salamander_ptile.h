@@ -126,12 +126,25 @@ __global__ __launch_bounds__(256, HY_PT_MIN_WAVES) void salamander_ptile_kernel(
     const bool staged = 16u * NB <= (uint32_t)HY_PT_LDS;
 
     if (wid == 0) {
-        // ---- output offsets: the tile prefix of the scan (256-datagram tiles) plus
-        // the widths of that scan tile's datagrams before p0
-        const uint64_t tb = p0 / kTile * kTile;
-        uint32_t pre = 0;
-        for (uint64_t q = tb + lane; q < p0; q += 64) pre += out_width<OBF>(pkt_len(B, q), B.pkt_cap);
-        const uint64_t base = uni64(B.tile_prefix[p0 / kTile] + wave_sum(pre));
+        // ---- keys on quads: lane 4k+i holds word i of datagram k's key.  The salt and
+        // offset loads are issued together, before the hash.
+        const uint32_t qk = lane >> 2, qi = lane & 3;
+        const uint64_t ioq = __shfl(io, (int)qk, 64);
+        const uint32_t Wq = __shfl(W0, (int)qk, 64);
+        uint64_t salt = 0;
+        if (qk < nt && (OBF || Wq)) salt = OBF ? B.salts[p0 + qk] : load8u(B.in + ioq);   // the wire's salt
+        // output offset of the tile: its scan tile's prefix plus its offset inside it
+        const uint64_t base = uni64(B.tile_prefix[p0 / kTile] + B.sub_prefix[p0 / kTileMaxD]);
+#if defined(HY_X_NOHASH) || defined(HY_X_TILE_NOHASH)   // ablation builds only (wrong output)
+        const uint64_t kw = salt * (qi + 3);
+#else
+        const uint64_t kw = quad_key<SW>(K, salt, qi);
+#endif
+        if (qk < nt) {
+            s_key[qk * 8 + qi] = kw;
+            s_key[qk * 8 + 4 + qi] = kw;
+            if (qi == 0) s_salt[qk] = salt;
+        }
         // drops: a region past out_cap is dropped, offsets unchanged (include/hyobfs.h)
         const uint32_t W = (W0 && base + os + W0 <= B.out_cap) ? W0 : 0u;
         if (mine) {
@@ -150,24 +163,6 @@ __global__ __launch_bounds__(256, HY_PT_MIN_WAVES) void salamander_ptile_kernel(
         if (B.out_total) {
             const uint64_t written = uni64(wave_sum(W));
             if (lane == 0 && written) atomicAdd(B.out_total, (unsigned long long)written);
-        }
-        // ---- keys on quads: lane 4k+i holds word i of datagram k's key
-        const uint32_t qk = lane >> 2, qi = lane & 3;
-        const uint32_t Lq = __shfl(L, (int)qk, 64);
-        const uint64_t ioq = __shfl(io, (int)qk, 64);
-        const uint32_t Wq = __shfl(W0, (int)qk, 64);
-        uint64_t salt = 0;
-        if (qk < nt && Wq) salt = OBF ? B.salts[p0 + qk] : load8u(B.in + ioq);   // the wire's salt
-        (void)Lq;
-#if defined(HY_X_NOHASH) || defined(HY_X_TILE_NOHASH)   // ablation builds only (wrong output)
-        const uint64_t kw = salt * (qi + 3);
-#else
-        const uint64_t kw = quad_key<SW>(K, salt, qi);
-#endif
-        if (qk < nt) {
-            s_key[qk * 8 + qi] = kw;
-            s_key[qk * 8 + 4 + qi] = kw;
-            if (qi == 0) s_salt[qk] = salt;
         }
     } else if (staged) {
         // ---- waves 1-3: the datagrams' input blocks into LDS, 1 KiB per instruction
@@ -195,6 +190,11 @@ __global__ __launch_bounds__(256, HY_PT_MIN_WAVES) void salamander_ptile_kernel(
     const uint32_t nch = (head + tend + 15) >> 4;
     uint8_t* __restrict__ ob = B.out + (base - head);
     const uint8_t* s_keyb = reinterpret_cast<const uint8_t*>(s_key);
+    // region starts in registers (lane d: datagram d, past nt: never reached)
+    const int32_t osl = lane < nt ? (int32_t)M.os[lane] : 0x7fffffff;
+    int32_t osd[kTileMaxD];
+#pragma unroll
+    for (int d = 1; d < (int)kTileMaxD; ++d) osd[d] = __builtin_amdgcn_readlane(osl, d);
     for (uint32_t c0 = 0; c0 < nch; c0 += 256u * U) {
         u128 r[U];
         uint32_t cov[U];
@@ -207,8 +207,7 @@ __global__ __launch_bounds__(256, HY_PT_MIN_WAVES) void salamander_ptile_kernel(
             const int32_t a = (int32_t)(16u * c) - (int32_t)head;   // tile-relative offset of chunk byte 0
             uint32_t k = 0;   // the last datagram whose region starts at or before a
 #pragma unroll
-            for (uint32_t step = 8; step; step >>= 1)
-                if (k + step < nt && (int32_t)M.os[k + step] <= a) k += step;
+            for (int d = 1; d < (int)kTileMaxD; ++d) k += osd[d] <= a ? 1u : 0u;
             const int32_t os = (int32_t)M.os[k], W = (int32_t)M.w[k];
             if (M.staged && W && os + (int32_t)SALT <= a && a + 16 <= os + W) {   // inside one payload
                 const int32_t jb = a - os - (int32_t)SALT;

@@ -25,8 +25,8 @@
 
 namespace hyobfs {
 
-constexpr int kTileMaxD = 16;        // datagrams per tile: one wave hashes 16 keys, 4 lanes each;
-                                     // 16 slots of a multiple of 8 bytes are whole 128-byte lines
+// kTileMaxD (kernels.h) datagrams per tile: one wave hashes 16 keys, 4 lanes each;
+// 16 slots of a multiple of 8 bytes are whole 128-byte lines
 constexpr uint64_t kMaxTileSlot = 1u << 20;
 #ifndef HY_TILE_MIN_WAVES
 #define HY_TILE_MIN_WAVES 8

@@ -1,0 +1,12 @@
+#!/bin/bash
+# Round 3: packed tile kernel with prepass sub-tile offsets -- GPU parity, in-process A/B against the wave kernel, bench line.
+set -e
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+O=gpurun_out/r03i
+mkdir -p $O
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest_gpu.log 2>&1
+for rep in 1 2; do
+  AB_WORKLOAD=bimodal timeout -k 10 300 python -u scripts/ab_variants.py auto,wave > $O/ab_bimodal_$rep.txt 2>&1
+done
+timeout -k 10 300 python -u bench.py > $O/bench.json 2> $O/bench.err
+echo done

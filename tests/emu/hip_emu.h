@@ -162,6 +162,8 @@ inline unsigned long long __ballot(int pred) {
 // convert it to unsigned first, exactly as on the GPU)
 inline int hyemu_readfirstlane(int v) { return hyemu::xchg(v, 0); }
 #define __builtin_amdgcn_readfirstlane(x) hyemu_readfirstlane((int)(x))
+inline int hyemu_readlane(int v, int l) { return hyemu::xchg(v, l); }
+#define __builtin_amdgcn_readlane(x, l) hyemu_readlane((int)(x), (int)(l))
 // DPP quad_perm only (dpp_ctrl 0x00-0xFF): lane i of each quad reads lane ctrl[i]
 inline int hyemu_mov_dpp(int v, int ctrl) {
     if (ctrl < 0 || ctrl > 0xFF) std::abort();

@@ -12,6 +12,9 @@ from concurrent.futures import ThreadPoolExecutor
 
 import pytest
 
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "emu"))
+from emu_build import ensure_emu_lib  # noqa: E402
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 EMU = os.path.join(ROOT, "tests", "emu")
 LIB = os.path.join(EMU, "libhyobfs_emu.so")
@@ -26,10 +29,7 @@ def _asan_runtime():
 def emu_lib():
     if not _asan_runtime() or not os.path.exists("/opt/rocm/llvm/bin/clang++"):
         pytest.skip("clang/ASan runtime not available")
-    srcs = glob.glob(os.path.join(ROOT, "hysteria_amd", "csrc", "*")) + [os.path.join(EMU, "hip_emu.h")]
-    if not os.path.exists(LIB) or os.path.getmtime(LIB) < max(os.path.getmtime(s) for s in srcs):
-        subprocess.run([os.path.join(EMU, "build.sh")], check=True, capture_output=True)
-    return LIB
+    return ensure_emu_lib()
 
 
 # Each test's case: (run_case.py arguments, extra environment), from its parameters.

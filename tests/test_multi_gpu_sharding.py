@@ -15,6 +15,9 @@ import sys
 import numpy as np
 import pytest
 
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "emu"))
+from emu_build import ensure_emu_lib  # noqa: E402
+
 from hysteria_amd.shard import byte_balanced_split, even_split, weak_shard
 from oracle import salamander_ref as ref
 
@@ -150,9 +153,7 @@ def test_gloo_two_ranks_emulated_product_shards(tmp_path):
     asan = sorted(glob.glob("/opt/rocm/llvm/lib/clang/*/lib/linux/libclang_rt.asan-x86_64.so"))
     if not asan or not os.path.exists("/opt/rocm/llvm/bin/clang++"):
         pytest.skip("clang/ASan runtime not available")
-    srcs = glob.glob(os.path.join(root, "hysteria_amd", "csrc", "*")) + [os.path.join(root, "tests", "emu", "hip_emu.h")]
-    if not os.path.exists(lib) or os.path.getmtime(lib) < max(os.path.getmtime(x) for x in srcs):
-        subprocess.run([os.path.join(root, "tests", "emu", "build.sh")], check=True, capture_output=True)
+    ensure_emu_lib()
     n = 2000
     _run_ranks("emu", n, tmp_path, extra_env={"HYOBFS_LIB": lib, "LD_PRELOAD": asan[-1],
                                               "ASAN_OPTIONS": "detect_leaks=0", "HYEMU_CUS": "2"})
