@@ -148,28 +148,28 @@ int64_t hyobfs_conn_read_from(hyobfs_conn* c, uint8_t* p, size_t cap, void* addr
     if (c->co) return hyobfs::coalescer_read(c->co, p, cap, addr, addrlen);
     for (;;) {
         std::lock_guard<std::mutex> lk(c->read_mu);
-        int flags = 0;
-        if (c->dl.read.load(std::memory_order_acquire)) {
-            // a read deadline: wait in slices of at most 50 ms, re-reading it (it
-            // may move while this call waits), then receive without blocking
-            for (;;) {
-                const int64_t d = c->dl.read.load(std::memory_order_acquire);
-                const int64_t left = d ? d - hyobfs::realtime_ns() : 50000000;
-                if (d && left <= 0) {
-                    errno = EAGAIN;
-                    return -1;
-                }
-                pollfd pf{c->fd, POLLIN, 0};
-                const int pr = poll(&pf, 1, (int)std::min<int64_t>(50, (left + 999999) / 1000000));
-                if (g.closed()) return -1;
-                if (pr > 0) break;
+        // wait in slices of at most 50 ms, re-reading the read deadline (it may be
+        // set or moved while this call waits: net.Conn deadlines apply to blocked
+        // calls too), then receive without blocking
+        for (;;) {
+            const int64_t d = c->dl.read.load(std::memory_order_acquire);
+            const int64_t left = d ? d - hyobfs::realtime_ns() : 50000000;
+            if (d && left <= 0) {
+                errno = EAGAIN;
+                return -1;
             }
-            flags = MSG_DONTWAIT;
+            pollfd pf{c->fd, POLLIN, 0};
+            const int pr = poll(&pf, 1, (int)std::min<int64_t>(50, (left + 999999) / 1000000));
+            if (g.closed()) return -1;
+            if (pr > 0) break;
+            if (pr < 0 && errno != EINTR) return -1;
         }
+        const int flags = MSG_DONTWAIT;
         socklen_t al = addrlen ? *addrlen : 0;
         const ssize_t n = recvfrom(c->fd, c->read_buf, kBuf, flags, static_cast<sockaddr*>(addr), addr ? &al : nullptr);
         if (addrlen) *addrlen = al;
         if (n <= 0 && g.closed()) return -1;   // woken by Close()
+        if (n < 0 && (errno == EAGAIN || errno == EWOULDBLOCK)) continue;   // readiness went stale: wait again
         if (n <= 0) return n;   // error or empty datagram: returned as is (:77-80)
         const size_t m = hyobfs_salamander_deobfuscate(c->ctx, c->read_buf, (size_t)n, p, cap);
         if (m > 0) return (int64_t)m;
