@@ -146,13 +146,20 @@ int64_t hyobfs_conn_read_from(hyobfs_conn* c, uint8_t* p, size_t cap, void* addr
     InFlight g(c);
     if (g.closed()) return -1;
     if (c->co) return hyobfs::coalescer_read(c->co, p, cap, addr, addrlen);
+    timeval tv{0, 0};
+    socklen_t tl = sizeof tv;
+    (void)getsockopt(c->fd, SOL_SOCKET, SO_RCVTIMEO, &tv, &tl);
+    const int64_t rcv_ns = (int64_t)tv.tv_sec * 1000000000ll + (int64_t)tv.tv_usec * 1000ll;
+    const int64_t rcv_limit = rcv_ns ? hyobfs::realtime_ns() + rcv_ns : 0;   // one limit for the whole call
     for (;;) {
         std::lock_guard<std::mutex> lk(c->read_mu);
         // wait in slices of at most 50 ms, re-reading the read deadline (it may be
         // set or moved while this call waits: net.Conn deadlines apply to blocked
-        // calls too), then receive without blocking
+        // calls too; without one, the socket's SO_RCVTIMEO read once bounds the
+        // call), then receive without blocking
         for (;;) {
-            const int64_t d = c->dl.read.load(std::memory_order_acquire);
+            int64_t d = c->dl.read.load(std::memory_order_acquire);
+            if (!d) d = rcv_limit;
             const int64_t left = d ? d - hyobfs::realtime_ns() : 50000000;
             if (d && left <= 0) {
                 errno = EAGAIN;
