@@ -165,19 +165,25 @@ __global__ __launch_bounds__(256, HY_PT_MIN_WAVES) void salamander_ptile_kernel(
             if (lane == 0 && written) atomicAdd(B.out_total, (unsigned long long)written);
         }
     } else if (staged) {
-        // ---- waves 1-3: the datagrams' input blocks into LDS, 1 KiB per instruction
+        // ---- waves 1-3: the datagrams' input blocks into LDS, 1 KiB per instruction.
+        // Block b belongs to the last datagram whose first block is <= b (block starts
+        // in scalar registers, no LDS round trips); its global block is b + delta.
+        const uint64_t dlt = (uint64_t)(ga >> 4) - bstart;
+        uint32_t bsd[kTileMaxD];
+        uint64_t dd[kTileMaxD];
+#pragma unroll
+        for (int d = 0; d < (int)kTileMaxD; ++d) {
+            bsd[d] = (uint32_t)__builtin_amdgcn_readlane((int)bstart, d);
+            dd[d] = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)dlt, d) |
+                    (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(dlt >> 32), d) << 32;
+        }
         for (uint32_t i = wid - 1; i * 64u < NB; i += 3) {
             const uint32_t b = i * 64u + lane;
-            uint32_t q = 0;   // datagram of block b: the last one whose first block is <= b
+            uint64_t delta = dd[0];
 #pragma unroll
-            for (uint32_t step = 8; step; step >>= 1) {
-                const uint32_t c = q + step;
-                const uint32_t bs = (uint32_t)__shfl(bstart, (int)min(c, 15u), 64);
-                if (c < nt && bs <= b) q = c;
-            }
-            const uint32_t bq = (uint32_t)__shfl(bstart, (int)q, 64);
-            const uintptr_t gq = (uintptr_t)__shfl((unsigned long long)ga, (int)q, 64);
-            if (b < NB) glds16(reinterpret_cast<const uint8_t*>(((gq >> 4) + (b - bq)) << 4), s_in + kPtSlack + 1024u * i);
+            for (int d = 1; d < (int)kTileMaxD; ++d)
+                if (bsd[d] <= b) delta = dd[d];
+            if (b < NB) glds16(reinterpret_cast<const uint8_t*>((b + delta) << 4), s_in + kPtSlack + 1024u * i);
         }
     }
     __syncthreads();   // every wave's LDS-DMA has landed (vmcnt(0)); keys and metadata are published

@@ -11,7 +11,8 @@ for rep in 1 2; do
   HYOBFS_GECKO_KERNEL=wave timeout -k 10 300 python -u scripts/aux_bench.py > $O/aux_wave_$rep.json 2> $O/aux_wave_$rep.err
 done
 for rep in 1 2; do
-  AB_WORKLOAD=bimodal timeout -k 10 300 python -u scripts/ab_variants.py auto,wave > $O/ab_bimodal_$rep.txt 2>&1
+  AB_LIBS="main=hysteria_amd/libhyobfs.so,prev=build_variants/libhyobfs_prev.so" AB_WORKLOAD=bimodal \
+    timeout -k 10 300 python -u scripts/ab_variants.py auto,wave > $O/ab_bimodal_$rep.txt 2>&1
 done
 timeout -k 10 300 python -u bench.py > $O/bench.json 2> $O/bench.err
 echo done
