@@ -13,12 +13,15 @@
 //   2. after one barrier, all four waves sweep the tile's wire range on the
 //      global 16-byte grid from a 64-byte aligned base, so the four lanes of a
 //      quad hold the four columns of one keystream block and compute it together
-//      (gk_ks_quad).  A chunk inside one frame's padding is its keystream column
-//      XOR 16 key bytes (an unaligned LDS read of the key stored twice in a row);
-//      one inside the chunk bytes is one unaligned 16-byte load of the message
-//      XOR the key; a chunk holding a salt, the header, a seam or a frame edge
-//      merges the frames touching it under byte masks.  Chunks shared with the
-//      neighbouring tiles and gaps between frames: masked stores.
+//      (gk_ks_quad).  The sweep takes the chunks inside one frame's padding (its
+//      keystream column XOR 16 key bytes: an unaligned LDS read of the key stored
+//      twice in a row) or inside its message bytes (one unaligned 16-byte load of
+//      the message XOR the key): every lane on the same path;
+//   3. then each frame's at most five other chunks (salt, header, the
+//      padding/message seam, the frame's end) are merged by one thread each,
+//      every frame touching the chunk under byte masks.  Chunks shared with the
+//      neighbouring tiles: masked stores.  (Merging those inside the sweep made
+//      every wave instruction run the merge for a few lanes: 2x slower.)
 // A tile whose valid frames are not in ascending, non-overlapping wire order, or
 // whose wire range has long gaps (more than kGtMaxRange bytes from the first
 // frame's start to the last frame's end), sweeps each frame's own range instead.
@@ -52,9 +55,10 @@ struct GtMeta {                      // the tile's valid frames in tile order (v
 
 // Frame v's bytes in the 16-byte chunk whose byte 0 is at offset a, the frame's
 // wire start being at rs (both relative to the same 64-aligned origin): salt,
-// then header / padding (ks: the chunk's keystream column) / chunk bytes, XOR the key.
+// then header / padding (ks(): the chunk's keystream column) / chunk bytes, XOR the key.
+template <class KS>
 __device__ __forceinline__ void gt_contrib(const hyobfs_gecko_batch& B, const GtMeta& M, const uint8_t* s_keyb,
-                                           uint32_t v, int32_t rs, int32_t a, gk_u128 ks, gk_u128& r,
+                                           uint32_t v, int32_t rs, int32_t a, KS&& ks, gk_u128& r,
                                            uint32_t& cov) {
     const uint32_t hpl = M.hpl[v];
     const int32_t hp = (int32_t)(hpl & 0xffff), plain = (int32_t)(hpl >> 16);
@@ -68,7 +72,7 @@ __device__ __forceinline__ void gt_contrib(const hyobfs_gecko_batch& B, const Gt
             X |= (p0 <= 0 ? H << (8 * -p0) : H >> (8 * p0)) & gk_mask(xlo - p0, hhi - p0);
         }
         const int32_t plo = max(p0, (int32_t)HYOBFS_GECKO_HEADER_LEN), phi = min(p0 + 16, hp);
-        if (plo < phi) X |= ks & gk_mask(plo - p0, phi - p0);   // padding
+        if (plo < phi) X |= ks() & gk_mask(plo - p0, phi - p0);   // padding
         const int32_t clo = max(p0, hp);
         if (clo < xhi) {   // chunk bytes
             const uint8_t* __restrict__ ch = B.msg + M.coff[v];
@@ -183,9 +187,10 @@ __global__ __launch_bounds__(256, HY_GT_MIN_WAVES) void gecko_tile_kernel(KeyPar
         int32_t rsd[kTileMaxD];
 #pragma unroll
         for (int d = 1; d < (int)kTileMaxD; ++d) rsd[d] = __builtin_amdgcn_readlane(rsl, d);
+        // ---- sweep: the chunks inside one frame's padding or message bytes
         for (uint32_t c0 = 0; c0 < nch; c0 += 256u * U) {
             gk_u128 r[U];
-            uint32_t cov[U];
+            bool ok[U];
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const uint32_t c = c0 + (uint32_t)u * 256u + tid;
@@ -201,32 +206,65 @@ __global__ __launch_bounds__(256, HY_GT_MIN_WAVES) void gecko_tile_kernel(KeyPar
                 const bool ichunk = in && p >= hp && p + 16 <= plain;
                 const bool ipad = in && p >= (int32_t)HYOBFS_GECKO_HEADER_LEN && p + 16 <= hp;
                 gk_u128 ks = 0;
-                if (__ballot(in && !ichunk))   // the whole wave: a quad computes one 64-byte block
+                if (__ballot(ipad))   // the whole wave: a quad computes one 64-byte block
 #ifdef HY_X_NOPAD   // ablation builds only (timing experiments; wrong output)
                     ks = (gk_u128)(base + 16ull * c);
 #else
                     ks = gk_ks_quad(P, (uint32_t)((base + 16ull * c) >> 6), lane & 3u);
 #endif
+                ok[u] = ichunk || ipad;
                 r[u] = 0;
-                cov[u] = 0;
-                if (ichunk || ipad) {
+                if (ok[u]) {
                     const gk_u128 X = ichunk ? gk_load16u(B.msg + M.coff[k] + (uint32_t)(p - hp)) : ks;
                     gk_u128 Kb;
                     __builtin_memcpy(&Kb, s_keyb + 64 * M.kix[k] + (uint32_t)(p & 31), 16);
                     r[u] = X ^ Kb;
-                    cov[u] = 0xFFFFu;
-                } else if (in) {   // salt, header, seam or edges: every frame touching the chunk
-                    for (uint32_t kk = k; kk < nv && (int32_t)M.rs[kk] < a + 16; ++kk)
-                        gt_contrib(B, M, s_keyb, kk, (int32_t)M.rs[kk], a, ks, r[u], cov[u]);
                 }
             }
 #pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const uint32_t c = c0 + (uint32_t)u * 256u + tid;
-                if (cov[u] == 0xFFFFu)
-                    store16_stream(ob + 16u * c, r[u]);
-                else if (cov[u])
-                    store_masked(ob + 16u * c, r[u], cov[u]);
+            for (int u = 0; u < U; ++u)
+                if (ok[u]) store16_stream(ob + 16u * (c0 + (uint32_t)u * 256u + tid), r[u]);
+        }
+        // ---- edges: a frame's other chunks are among five (salt and header: 13 bytes,
+        // at most two chunks; the last chunk holding padding or header and the first
+        // holding message bytes; the last).  Thread e takes candidate e % 5 of frame
+        // e / 5; the first frame touching a chunk merges every frame touching it.
+        if (tid < 5u * nv) {
+            const uint32_t v = tid / 5u, w = tid % 5u;
+            const int32_t rs = (int32_t)M.rs[v];
+            const uint32_t hpl = M.hpl[v];
+            const int32_t hp = (int32_t)(hpl & 0xffff), plain = (int32_t)(hpl >> 16);
+            const int32_t E = rs + (int32_t)HYOBFS_SALT_LEN + plain;
+            auto cand = [&](uint32_t i) -> int32_t {
+                const int32_t x = i == 0 ? rs : i == 1 ? rs + 12 : i == 2 ? rs + 7 + hp : i == 3 ? rs + 8 + hp : E - 1;
+                return x >> 4;
+            };
+            const int32_t c = cand(w), a = 16 * c;
+            bool skip = a >= E;   // no message bytes: candidate 3 may lie past the frame
+#pragma unroll
+            for (uint32_t i = 0; i < 4; ++i) skip = skip || (i < w && cand(i) == c);
+            const int32_t p = a - rs - (int32_t)HYOBFS_SALT_LEN;
+            skip = skip || (p >= hp && p + 16 <= plain) || (p >= (int32_t)HYOBFS_GECKO_HEADER_LEN && p + 16 <= hp);
+            // frames are ascending: only the previous one can reach into the chunk
+            skip = skip || (v > 0 && (int32_t)(M.rs[v - 1] + HYOBFS_SALT_LEN + (M.hpl[v - 1] >> 16)) > a);
+            if (!skip) {
+                gk_u128 r = 0, ksv = 0;
+                uint32_t cov = 0;
+                bool have = false;
+                auto ks = [&]() -> gk_u128 {   // this chunk's keystream column, one lane alone
+                    if (!have) {
+                        const uint64_t g = base + (uint64_t)a;
+                        ksv = gk_ks_single(P, (uint32_t)(g >> 6), (uint32_t)(g >> 4) & 3u);
+                        have = true;
+                    }
+                    return ksv;
+                };
+                for (uint32_t kk = v; kk < nv && (int32_t)M.rs[kk] < a + 16; ++kk)
+                    gt_contrib(B, M, s_keyb, kk, (int32_t)M.rs[kk], a, ks, r, cov);
+                if (cov == 0xFFFFu)
+                    store16_stream(ob + a, r);
+                else if (cov)
+                    store_masked(ob + a, r, cov);
             }
         }
         return;
@@ -243,7 +281,7 @@ __global__ __launch_bounds__(256, HY_GT_MIN_WAVES) void gecko_tile_kernel(KeyPar
             if (j < n) {
                 gk_u128 r = 0;
                 uint32_t cov = 0;
-                gt_contrib(B, M, s_keyb, v, rs, (int32_t)(16u * j), ks, r, cov);
+                gt_contrib(B, M, s_keyb, v, rs, (int32_t)(16u * j), [&] { return ks; }, r, cov);
                 if (cov == 0xFFFFu)
                     store16_stream(B.out + A0 + 16u * j, r);
                 else if (cov)

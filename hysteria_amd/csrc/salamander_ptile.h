@@ -12,13 +12,15 @@
 //      plus the widths of the scan tile's earlier datagrams), the widths and
 //      drop rules (salamander.go:60-62, :75-77), loads the 16 salts and hashes the
 //      16 keys on quads (salamander_tile.h quad_key), all into LDS;
-//   3. after one barrier, all four waves compose the tile's output range in
-//      16-byte chunks on the global 16-byte grid, 1 KiB per wave instruction: a
-//      chunk inside one payload is one unaligned 16-byte LDS read of the staged
-//      input, one of the key (stored twice in a row, so any 16 key bytes are
-//      contiguous), an XOR and a store; a chunk holding salts or datagram edges
-//      merges the few datagrams touching it under byte masks.  The first and last
-//      chunks of a tile are shared with the neighbouring tiles: masked stores.
+//   3. after one barrier, all four waves sweep the tile's output range in 16-byte
+//      chunks on the global 16-byte grid, 1 KiB per wave instruction: a chunk
+//      inside one payload is one unaligned 16-byte LDS read of the staged input,
+//      one of the key (stored twice in a row, so any 16 key bytes are contiguous),
+//      an XOR and a store;
+//   4. then each datagram's two or three other chunks (salt, edges) are merged by
+//      one thread each, every datagram touching the chunk under byte masks.  The
+//      first and last chunks of a tile are shared with the neighbouring tiles:
+//      masked stores.
 // A tile whose staged input would not fit the LDS budget (datagrams of more than
 // ~1.2 KiB on average) reads its inputs from global memory in the same compose
 // step instead (16-byte windows, as the wave kernel does).
@@ -201,41 +203,67 @@ __global__ __launch_bounds__(256, HY_PT_MIN_WAVES) void salamander_ptile_kernel(
     int32_t osd[kTileMaxD];
 #pragma unroll
     for (int d = 1; d < (int)kTileMaxD; ++d) osd[d] = __builtin_amdgcn_readlane(osl, d);
+    // ---- sweep: the chunks inside one payload (every lane on the same path)
+    const bool stg = M.staged != 0;
     for (uint32_t c0 = 0; c0 < nch; c0 += 256u * U) {
         u128 r[U];
-        uint32_t cov[U];
+        bool ok[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const uint32_t c = c0 + (uint32_t)u * 256u + tid;
-            r[u] = 0;
-            cov[u] = 0;
-            if (c >= nch) continue;
             const int32_t a = (int32_t)(16u * c) - (int32_t)head;   // tile-relative offset of chunk byte 0
             uint32_t k = 0;   // the last datagram whose region starts at or before a
 #pragma unroll
             for (int d = 1; d < (int)kTileMaxD; ++d) k += osd[d] <= a ? 1u : 0u;
             const int32_t os = (int32_t)M.os[k], W = (int32_t)M.w[k];
-            if (M.staged && W && os + (int32_t)SALT <= a && a + 16 <= os + W) {   // inside one payload
+            ok[u] = c < nch && W && os + (int32_t)SALT <= a && a + 16 <= os + W;
+            r[u] = 0;
+            if (ok[u]) {
                 const int32_t jb = a - os - (int32_t)SALT;
                 u128 V, Kb;
-                __builtin_memcpy(&V, s_in + (int32_t)(M.src[k] + (OBF ? 0u : 8u)) + jb, 16);
+                if (stg)
+                    __builtin_memcpy(&V, s_in + (int32_t)(M.src[k] + (OBF ? 0u : 8u)) + jb, 16);
+                else
+                    V = load16u(B.in + M.io[k] + (OBF ? 0u : 8u) + (uint32_t)jb);
                 __builtin_memcpy(&Kb, s_keyb + 64 * k + (uint32_t)(jb & 31), 16);
                 r[u] = V ^ Kb;
-                cov[u] = 0xFFFFu;
-                continue;
             }
-            // edges: every datagram touching the chunk (the one before k may reach into it
-            // only if it ends after a: k is the last region starting at or before a)
-            for (uint32_t kk = k; kk < nt && (int32_t)M.os[kk] < a + 16; ++kk)
-                pt_contrib<OBF>(B, M, s_in, s_keyb, s_salt, kk, a, r[u], cov[u]);
         }
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const uint32_t c = c0 + (uint32_t)u * 256u + tid;
-            if (cov[u] == 0xFFFFu)
+        for (int u = 0; u < U; ++u)
+            if (ok[u]) {
+                const uint32_t c = c0 + (uint32_t)u * 256u + tid;
                 store16_global(ob + 16u * c, (uint64_t)r[u], (uint64_t)(r[u] >> 64));
-            else if (cov[u])
-                store_masked(ob + 16u * c, r[u], cov[u]);
+            }
+    }
+    // ---- edges: a region's other chunks are its first, the one holding its last salt
+    // byte (obfuscate) and its last.  Thread e takes candidate e % NC of datagram e / NC;
+    // the first region touching a chunk merges every region touching it.  (Merging
+    // inside the sweep made every wave instruction run the merge for a few lanes.)
+    constexpr uint32_t NC = OBF ? 3u : 2u;
+    if (tid < NC * nt) {
+        const uint32_t v = tid / NC, w = tid % NC;
+        const int32_t os = (int32_t)M.os[v], W = (int32_t)M.w[v];
+        auto cand = [&](uint32_t i) -> int32_t {   // chunk index on the tile's grid
+            const int32_t x = i == 0 ? os : (i == NC - 1 ? os + W - 1 : os + 7);
+            return (x + (int32_t)head) >> 4;
+        };
+        const int32_t c = cand(w), a = 16 * c - (int32_t)head;
+        bool skip = W == 0 || (w > 0 && cand(0) == c) || (w == 2 && cand(1) == c) ||
+                    (os + (int32_t)SALT <= a && a + 16 <= os + W);   // inside the payload: the sweep's
+        // an earlier region reaching into the chunk owns it (regions are back to back:
+        // region u ends at or before os[u + 1])
+        for (int32_t u = (int32_t)v - 1; !skip && u >= 0 && (int32_t)M.os[u + 1] > a; --u)
+            skip = M.w[u] && (int32_t)(M.os[u] + M.w[u]) > a;
+        if (!skip) {
+            u128 r = 0;
+            uint32_t cov = 0;
+            for (uint32_t kk = v; kk < nt && (int32_t)M.os[kk] < a + 16; ++kk)
+                pt_contrib<OBF>(B, M, s_in, s_keyb, s_salt, kk, a, r, cov);
+            if (cov == 0xFFFFu)
+                store16_global(ob + 16 * c, (uint64_t)r, (uint64_t)(r >> 64));
+            else if (cov)
+                store_masked(ob + 16 * c, r, cov);
         }
     }
 }

@@ -185,7 +185,8 @@ def case_gecko(n_msgs, seed, layout=0):
     """Gecko frames: one device encode pass vs oracle/gecko_ref, then deobfuscate + parse.
     layout 0: packed wire order (the aligned sweep); 1: ascending with gaps between
     frames (aligned sweep, gap bytes untouched); 2: frames placed in shuffled order
-    (the plaintext-window path)."""
+    (the per-frame path); 3: tiny frames packed back to back (0..40 pad bytes,
+    1..20 message bytes: several frames per 16-byte chunk)."""
     from hysteria_amd import gecko
     from oracle import gecko_ref as gref
     psk = b"average_password"
@@ -195,7 +196,17 @@ def case_gecko(n_msgs, seed, layout=0):
     msg = rng.integers(0, 256, int(lens.sum()) + 16, dtype=np.uint8)
     fr, off, total = gecko.plan_fragments(lens, 400, 900, first_msg_id=seed)
     nf = len(fr)
-    if layout:
+    if layout == 3:
+        nf = n_msgs
+        cl = rng.integers(1, 21, nf)
+        pl = rng.choice([0, 1, 2, 3, 17, 40], nf)
+        tot = rng.integers(2, 9, nf)
+        fr = np.array([(int(rng.integers(0, len(msg) - 24)), int(cl[i]), int(pl[i]), i & 0xff,
+                        int(rng.integers(0, tot[i])) << 4 | int(tot[i])) for i in range(nf)], dtype=gecko.FRAME_DTYPE)
+        w = (13 + cl + pl).astype(np.uint64)
+        off = np.concatenate([[5], 5 + np.cumsum(w)[:-1]]).astype(np.uint64)
+        total = int(5 + w.sum())
+    elif layout:
         widths = np.diff(np.append(off, total)).astype(np.uint64)
         order = rng.permutation(nf) if layout == 2 else np.arange(nf)
         gaps = rng.integers(0, 41, nf).astype(np.uint64) if layout == 1 else np.zeros(nf, np.uint64)

@@ -108,7 +108,8 @@ CASES = [
     ("far", "200 300 15 0", "8"),
     ("gecko", "40 7", "2"),              # Gecko frame encode + parse kernels (gecko.hip), aligned sweep
     ("gecko", "60 8 1", "2"),            # ... ascending frames with gaps: gap bytes untouched
-    ("gecko", "60 9 2", "2"),            # ... shuffled placement: the plaintext-window path
+    ("gecko", "60 9 2", "2"),            # ... shuffled placement: the per-frame path
+    ("gecko", "70 10 3", "2"),           # ... tiny frames, several per 16-byte chunk
     ("punch", "300 5 3", "2"),           # realm punch matcher (realm.hip)
     ("quic", "2", "2"),                  # QUIC Initial unprotect + ReadCryptoPayload kernels (quic.hip)
 ]
