@@ -439,6 +439,9 @@ HY_EXTERN_GT(14) HY_EXTERN_GT(15)
 hipError_t launch_gecko_encode(const KeyParams& k, const hyobfs_gecko_batch& b, hipStream_t s) {
     if (b.n == 0) return hipSuccess;
     static const bool wave = [] {
+#ifdef HY_GK_FORCE_WAVE   // A/B builds: the wave-group kernel in every process
+        return true;
+#endif
         const char* e = std::getenv("HYOBFS_GECKO_KERNEL");
         return e && std::strcmp(e, "wave") == 0;
     }();

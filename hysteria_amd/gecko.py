@@ -90,8 +90,8 @@ PARSED_DTYPE = np.dtype([("status", "<i4"), ("pad_len", "<u2"), ("msg_id", "u1")
 assert FRAME_DTYPE.itemsize == 16 and PARSED_DTYPE.itemsize == 16
 
 
-def _glib():
-    lib = _lib.load()
+def _glib(lib=None):
+    lib = lib or _lib.load()
     if not getattr(lib, "_gecko_declared", False):
         vp, sz, u64, i32, u32 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_int, ctypes.c_uint32
         hp = ctypes.POINTER(HyobfsGeckoHeader)
@@ -414,7 +414,8 @@ def encode_batch(obfuscator, *, msg, frames, salts, out, out_off, pad_key: bytes
                          pad_key=(ctypes.c_uint8 * 32).from_buffer_copy(pad_key),
                          pad_nonce=(ctypes.c_uint8 * 12).from_buffer_copy(pad_nonce),
                          out=_ptr(out), out_off=_ptr(out_off), workspace=_ptr(workspace), workspace_bytes=ws_bytes)
-    check(_glib().hyobfs_gecko_encode_batch(obfuscator._h, ctypes.byref(b), _stream(stream, out)), "gecko_encode_batch")
+    lib = _glib(getattr(obfuscator, "_lib", None))   # the library the context came from
+    check(lib.hyobfs_gecko_encode_batch(obfuscator._h, ctypes.byref(b), _stream(stream, out)), "gecko_encode_batch")
 
 
 def parse_batch(inp, in_off, in_len, n: int, out, stream=None) -> None:
