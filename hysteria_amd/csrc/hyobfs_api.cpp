@@ -588,8 +588,7 @@ size_t hyobfs_salamander_deobfuscate(hyobfs_salamander* c, const uint8_t* in, si
 
 uint64_t hyobfs_batch_workspace_size(uint64_t n) {
     const uint64_t ntiles = (n + hyobfs::kTile - 1) / hyobfs::kTile;
-    const uint64_t nsub = (n + hyobfs::kTileMaxD - 1) / hyobfs::kTileMaxD;
-    return (ntiles + 1 + nsub) * sizeof(uint64_t);
+    return (ntiles + 1) * sizeof(uint64_t);
 }
 
 int hyobfs_salamander_obfuscate_batch(hyobfs_salamander* c, const hyobfs_batch* b, void* stream) {

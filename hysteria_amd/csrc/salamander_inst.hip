@@ -1,7 +1,6 @@
-// salamander_inst.hip -- instantiates the batch kernels (Salamander, Gecko tile) for one salt word
+// salamander_inst.hip -- instantiates the batch kernels for one salt word
 // (compiled once per HY_SW = 0..15, see Makefile).
-#include "salamander_ptile.h"
-#include "gecko_tile.h"
+#include "salamander_tile.h"
 
 #ifndef HY_SW
 #error "compile with -DHY_SW=<salt word 0..15>"
@@ -14,7 +13,4 @@ template void launch_wave_sw<false, true, HY_SW>(const BatchParams&, const KeyPa
 template void launch_wave_sw<false, false, HY_SW>(const BatchParams&, const KeyParams&, hipStream_t);
 template void launch_tile_sw<true, HY_SW>(const BatchParams&, const KeyParams&, const TileParams&, hipStream_t);
 template void launch_tile_sw<false, HY_SW>(const BatchParams&, const KeyParams&, const TileParams&, hipStream_t);
-template void launch_ptile_sw<true, HY_SW>(const BatchParams&, const KeyParams&, hipStream_t);
-template void launch_ptile_sw<false, HY_SW>(const BatchParams&, const KeyParams&, hipStream_t);
-template void launch_gecko_tile_sw<HY_SW>(const KeyParams&, const hyobfs_gecko_batch&, hipStream_t);
 }  // namespace hyobfs

@@ -186,8 +186,6 @@ typedef struct hyobfs_batch {
     uint64_t workspace_bytes;
 } hyobfs_batch;
 
-/* Packed-layout scratch: 8 bytes per 256 datagrams (+8) for the scan's tile
- * sums and 8 bytes per 16 datagrams for the tile offsets inside them. */
 uint64_t hyobfs_batch_workspace_size(uint64_t n);
 int hyobfs_salamander_obfuscate_batch(hyobfs_salamander* ctx, const hyobfs_batch* b,
                                       void* stream);

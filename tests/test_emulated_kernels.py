@@ -34,7 +34,7 @@ def emu_lib():
 
 # Each test's case: (run_case.py arguments, extra environment), from its parameters.
 SPECS = {
-    "test_emulated_ptile_kernel": lambda p: (p["which"], p["args"], {"HYEMU_CUS": "2"}),
+    "test_emulated_packed_auto": lambda p: (p["which"], p["args"], {"HYEMU_CUS": "2"}),
     "test_emulated_tile_kernel": lambda p: (p["which"], p["args"], {"HYOBFS_KERNEL": "tile", "HYEMU_CUS": "2"}),
     "test_emulated_wave_kernel_forced": lambda p: None if p["which"] in ("conn", "host", "coalesce", "quic",
                                                                          "lifecycle", "deadline") else (
@@ -130,11 +130,10 @@ RUN_CASES = [
 ]
 
 
-# The packed tile kernel (salamander_ptile.h, every packed batch under AUTO): tiny
-# datagrams (several per 16-byte chunk, empty ones), ragged 1-2 KiB, tiles too large
-# for the LDS budget (inputs read from global memory), out_cap cutting the batch,
-# deobfuscate of real wire with drops (wire of 8 bytes), PSK lengths across salt words.
-PTILE_CASES = [
+# Packed batches under AUTO (the wave kernel): tiny datagrams (several per 16-byte
+# chunk, empty ones), ragged 1-6 KiB, out_cap cutting the batch, deobfuscate of real
+# wire with drops (wire of 8 bytes), PSK lengths across salt words.
+PACKED_CASES = [
     ("pcap", "1 300 40 1 100 16"), ("pcap", "2 300 40 0 100 16"), ("pcap", "3 400 2100 1 100 9"),
     ("pcap", "4 400 2100 0 100 121"), ("pcap", "5 200 6000 1 100 16"), ("pcap", "6 200 6000 0 100 33"),
     ("pcap", "7 500 1400 1 60 16"), ("pcap", "8 500 1400 0 70 127"), ("pcap", "9 17 3 1 100 4"),
@@ -142,8 +141,8 @@ PTILE_CASES = [
 ]
 
 
-@pytest.mark.parametrize("which,args", PTILE_CASES)
-def test_emulated_ptile_kernel(emu_lib, which, args):
+@pytest.mark.parametrize("which,args", PACKED_CASES)
+def test_emulated_packed_auto(emu_lib, which, args):
     _run(emu_lib, which, args, {"HYEMU_CUS": "2"})
 
 
