@@ -12,13 +12,15 @@
 // gk_ks_quad), each leaves as one 16-byte store.  Then lane l merges frame l's few edge windows
 // (header, padding/chunk seam, frame end) under byte masks; keeping them out of
 // the sweep keeps its lanes on the same path.  Lane l hashes frame l's key
-// (BLAKE2b-256, salamander_device.h) in registers in step 1, so the hash overlaps
-// other waves' sweeps (a separate keys_kernel pass via the workspace was 15 % slower).
+// (BLAKE2b-256, wave_key<SW> of salamander_wave.h: one instantiation per salt word)
+// in registers in step 1, so the hash overlaps other waves' sweeps (a separate
+// keys_kernel pass via the workspace was 15 % slower).
 //
 // Parse: one thread per deobfuscated datagram, the checks of ReadFrom
 // (gecko.go:170-193) and decodeFrame (gecko_frame.go:65-86) in their order.
 #include "kernels.h"
 #include "salamander_device.h"
+#include "salamander_wave.h"   // wave_key<SW>: the key unrolled per salt word
 #include "../../include/hyobfs_gecko.h"
 
 namespace hyobfs {
@@ -289,11 +291,19 @@ __device__ __forceinline__ void gecko_encode_aligned(const KeyParams& K, const h
     }
 }
 
-#ifdef HY_GK_WPE   // A/B builds only: register cap for the fused hash
-#define HY_GK_ATTR __attribute__((amdgpu_waves_per_eu(HY_GK_WPE)))
-#else
-#define HY_GK_ATTR
+// Register cap: 6 waves/SIMD (80 VGPRs, a few spilled around the hash) measured fastest
+// with the per-salt-word key: 0.561 ms against 0.567 at 5 waves (94 VGPRs), 0.623 for the
+// generic key at 4 waves (97 VGPRs) and 0.734 at 8 waves (heavy spills),
+// profiles/r03_ab_gecko_occupancy.txt.
+#ifndef HY_GK_WPE
+#define HY_GK_WPE 6
 #endif
+#ifdef HYOBFS_EMULATE
+#define HY_GK_ATTR
+#else
+#define HY_GK_ATTR __attribute__((amdgpu_waves_per_eu(HY_GK_WPE)))
+#endif
+template <int SW>
 __global__ __launch_bounds__(256) HY_GK_ATTR void gecko_encode_kernel(KeyParams K, hyobfs_gecko_batch B) {
     __shared__ GeckoGroup gg[4];
     const uint32_t lane = threadIdx.x & 63;
@@ -323,16 +333,11 @@ __global__ __launch_bounds__(256) HY_GK_ATTR void gecko_encode_kernel(KeyParams 
                           (uint64_t)(fr.pad_len & 0xff) << 32;
             G.hp_plain[lane] = hp | plain << 16;
             salt = B.salts[f];
-#ifdef HY_GK_KEYS_KERNEL   // A/B builds only: keys from keys_kernel via the workspace
-            const uint8_t* kp = static_cast<const uint8_t*>(B.workspace) + 32 * f;
-            __builtin_memcpy(&k0, kp, 16);
-            __builtin_memcpy(&k1, kp + 16, 16);
-#else   // keyLocked (salamander.go:88-91) in registers; the hash overlaps other waves' sweeps
+            // keyLocked (salamander.go:88-91) in registers; the hash overlaps other waves' sweeps
             uint64_t kw[4];
-            salamander_key(K, salt, kw);
+            wave_key<SW>(K, salt, kw);
             k0 = (gk_u128)kw[1] << 64 | kw[0];
             k1 = (gk_u128)kw[3] << 64 | kw[2];
-#endif
         }
     }
     // Aligned path when the group's valid frames are in ascending, non-overlapping
@@ -537,17 +542,16 @@ __global__ __launch_bounds__(256) void gecko_parse_kernel(const uint8_t* in, con
 
 hipError_t launch_gecko_encode(const KeyParams& k, const hyobfs_gecko_batch& b, hipStream_t s) {
     if (b.n == 0) return hipSuccess;
-#ifdef HY_GK_KEYS_KERNEL
-    hipError_t e = launch_keys(k, b.salts, static_cast<uint8_t*>(b.workspace), b.n, s);
-    if (e != hipSuccess) return e;
-#endif
-    // (Instantiating per salt word as the wave kernel does cuts 96 -> 60 VGPRs, 5 -> 8
-    // waves/SIMD, and measured 4 % slower: profiles/r01_ab_gecko/.)
-    static const uint32_t lds_pad = [] {   // A/B only: unused dynamic LDS to cap workgroups per CU
-        const char* e = std::getenv("HYOBFS_GK_LDS_PAD");
-        return e ? (uint32_t)std::atoi(e) : 0u;
-    }();
-    hipLaunchKernelGGL(gecko_encode_kernel, dim3((uint32_t)((b.n + 255) / 256)), dim3(256), lds_pad, s, k, b);
+    // instantiated per salt word (salamander_inst.hip's rule): the PSK's message words
+    // stay scalar, only the salt's one or two words are per lane
+    const dim3 grid((uint32_t)((b.n + 255) / 256)), block(256);
+    switch (k.salt_pos >> 3) {
+#define HY_CASE(n) \
+    case n: hipLaunchKernelGGL(gecko_encode_kernel<n>, grid, block, 0, s, k, b); break;
+        HY_CASE(0) HY_CASE(1) HY_CASE(2) HY_CASE(3) HY_CASE(4) HY_CASE(5) HY_CASE(6) HY_CASE(7)
+        HY_CASE(8) HY_CASE(9) HY_CASE(10) HY_CASE(11) HY_CASE(12) HY_CASE(13) HY_CASE(14) HY_CASE(15)
+#undef HY_CASE
+    }
     return hipGetLastError();
 }
 
