@@ -508,7 +508,7 @@ void hyobfs_salamander_free(hyobfs_salamander* c) {
 int hyobfs_salamander_device(const hyobfs_salamander* c) { return c ? c->device : -1; }
 
 int hyobfs_salamander_set_kernel(hyobfs_salamander* c, int kernel) {
-    if (!c || kernel < HYOBFS_KERNEL_AUTO || kernel > HYOBFS_KERNEL_PACKED) return HYOBFS_ERR_INVALID;
+    if (!c || kernel < HYOBFS_KERNEL_AUTO || kernel > HYOBFS_KERNEL_TILE) return HYOBFS_ERR_INVALID;
     c->kernel = kernel;
     return HYOBFS_OK;
 }
@@ -588,8 +588,7 @@ size_t hyobfs_salamander_deobfuscate(hyobfs_salamander* c, const uint8_t* in, si
 
 uint64_t hyobfs_batch_workspace_size(uint64_t n) {
     const uint64_t ntiles = (n + hyobfs::kTile - 1) / hyobfs::kTile;
-    const uint64_t nsub = (n + hyobfs::kTileMaxD - 1) / hyobfs::kTileMaxD;
-    return (ntiles + 1 + nsub) * sizeof(uint64_t);
+    return (ntiles + 1) * sizeof(uint64_t);
 }
 
 int hyobfs_salamander_obfuscate_batch(hyobfs_salamander* c, const hyobfs_batch* b, void* stream) {

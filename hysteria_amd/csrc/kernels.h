@@ -29,11 +29,10 @@ __device__ __forceinline__ void hy_wave_sync() {
 #endif
 
 constexpr int kTile = 256;          // datagrams per tile-sum entry of the packed layout's scan
-constexpr int kTileMaxD = 16;       // datagrams per tile of the tile kernels (salamander_tile.h)
 constexpr uint32_t kMaxDatagram = (1u << 24) - 64;  // longest datagram a batch accepts
 constexpr uint64_t kMaxStride = 1ull << 24;         // longest slot of a slotted output
 // batch kernels (include/hyobfs.h HYOBFS_KERNEL_*)
-constexpr int kKernelAuto = 0, kKernelWave = 1, kKernelTile = 2, kKernelPacked = 3;
+constexpr int kKernelAuto = 0, kKernelWave = 1, kKernelTile = 2;
 
 // BLAKE2b state for the per-packet key, precomputed on the host from the PSK
 // alone (salamander.go:88-91 hashes PSK || salt; every block before the one
@@ -64,8 +63,7 @@ struct BatchParams {
     uint32_t* out_len;
     unsigned long long* out_total;
     const uint64_t* tile_prefix;  // packed: exclusive prefix of tile sums (ntiles+1)
-    uint64_t* tile_sums;          // packed: scratch, ntiles+1 entries, then sub_prefix
-    uint64_t* sub_prefix;         // packed: per 16-datagram tile, its offset inside its scan tile
+    uint64_t* tile_sums;          // packed: scratch, ntiles+1 entries
     uint32_t run_log2;            // wave kernel: datagrams per run = 2^run_log2
     int kernel;                   // HYOBFS_KERNEL_* of the context (0 = auto)
 };

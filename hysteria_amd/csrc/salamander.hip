@@ -13,7 +13,7 @@
 //     One-shot workgroups of 16 datagrams: a key wave beside three data waves.
 //   * salamander_wave_kernel (salamander_wave.h): every other layout (packed
 //     output, ragged lengths, any alignment).  One wave per 64-datagram group.
-#include "salamander_packed.h"
+#include "salamander_tile.h"
 
 namespace hyobfs {
 
@@ -26,33 +26,24 @@ namespace hyobfs {
     extern template void launch_tile_sw<true, n>(const BatchParams&, const KeyParams&, const TileParams&,   \
                                                  hipStream_t);                                              \
     extern template void launch_tile_sw<false, n>(const BatchParams&, const KeyParams&, const TileParams&,  \
-                                                  hipStream_t);                                              \
-    extern template void launch_packed_sw<true, n>(const BatchParams&, const KeyParams&, hipStream_t);      \
-    extern template void launch_packed_sw<false, n>(const BatchParams&, const KeyParams&, hipStream_t);
+                                                  hipStream_t);
 HY_EXTERN_SW(0) HY_EXTERN_SW(1) HY_EXTERN_SW(2) HY_EXTERN_SW(3) HY_EXTERN_SW(4) HY_EXTERN_SW(5)
 HY_EXTERN_SW(6) HY_EXTERN_SW(7) HY_EXTERN_SW(8) HY_EXTERN_SW(9) HY_EXTERN_SW(10) HY_EXTERN_SW(11)
 HY_EXTERN_SW(12) HY_EXTERN_SW(13) HY_EXTERN_SW(14) HY_EXTERN_SW(15)
 #undef HY_EXTERN_SW
 
 // ------------------------------------------------------ packed-layout scan
-// Tile sums of the output widths (256-datagram scan tiles), and for each
-// 16-datagram tile its offset inside its scan tile (the packed kernel's base).
+// Tile sums of the output widths; the main kernel adds a wavefront scan.
 template <bool OBF>
 __global__ __launch_bounds__(kTile) void tile_sums_kernel(BatchParams B) {
     __shared__ uint64_t s_w[kTile / 64];
-    const uint32_t t = threadIdx.x, lane = t & 63;
-    const uint64_t p = (uint64_t)blockIdx.x * kTile + t;
+    const uint64_t p = (uint64_t)blockIdx.x * kTile + threadIdx.x;
     uint32_t W = 0;
     if (p < B.n) W = out_width<OBF>(pkt_len(B, p), B.pkt_cap);
-    const uint64_t inc = wave_incl_scan((uint64_t)W, (int)lane);
-    if (lane == 63) s_w[t >> 6] = inc;
+    const uint64_t ws = wave_sum(W);
+    if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = ws;
     __syncthreads();
-    if ((t & (kTileMaxD - 1)) == 0 && p < B.n) {
-        uint64_t pre = inc - W;
-        for (uint32_t w = 0; w < (t >> 6); ++w) pre += s_w[w];
-        B.sub_prefix[p / kTileMaxD] = pre;
-    }
-    if (t == 0) {
+    if (threadIdx.x == 0) {
         uint64_t s = 0;
 #pragma unroll
         for (int i = 0; i < kTile / 64; ++i) s += s_w[i];
@@ -162,11 +153,8 @@ static int kernel_override() {   // HYOBFS_KERNEL, as HYOBFS_KERNEL_* (0 = auto)
     static int v = -1;
     if (v == -1) {
         const char* e = std::getenv("HYOBFS_KERNEL");
-        v = !e                              ? kKernelAuto
-            : std::strcmp(e, "wave") == 0   ? kKernelWave
-            : std::strcmp(e, "tile") == 0   ? kKernelTile
-            : std::strcmp(e, "packed") == 0 ? kKernelPacked
-                                            : kKernelAuto;
+        v = !e ? kKernelAuto : std::strcmp(e, "wave") == 0 ? kKernelWave : std::strcmp(e, "tile") == 0 ? kKernelTile
+                                                                                                     : kKernelAuto;
     }
     return v;
 }
@@ -181,17 +169,6 @@ static void launch_main(const BatchParams& bp, const KeyParams& k, hipStream_t s
         switch (k.salt_pos >> 3) {
 #define HY_CASE(n) \
     case n: launch_tile_sw<OBF, n>(bp, k, T, s); break;
-            HY_CASE(0) HY_CASE(1) HY_CASE(2) HY_CASE(3) HY_CASE(4) HY_CASE(5) HY_CASE(6) HY_CASE(7)
-            HY_CASE(8) HY_CASE(9) HY_CASE(10) HY_CASE(11) HY_CASE(12) HY_CASE(13) HY_CASE(14)
-            HY_CASE(15)
-#undef HY_CASE
-        }
-        return;
-    }
-    if (PACKED && kc == kKernelPacked) {   // opt-in: the pipelined packed kernel
-        switch (k.salt_pos >> 3) {
-#define HY_CASE(n) \
-    case n: launch_packed_sw<OBF, n>(bp, k, s); break;
             HY_CASE(0) HY_CASE(1) HY_CASE(2) HY_CASE(3) HY_CASE(4) HY_CASE(5) HY_CASE(6) HY_CASE(7)
             HY_CASE(8) HY_CASE(9) HY_CASE(10) HY_CASE(11) HY_CASE(12) HY_CASE(13) HY_CASE(14)
             HY_CASE(15)
@@ -217,7 +194,6 @@ hipError_t launch_salamander(bool obf, const BatchParams& b, const KeyParams& k,
     BatchParams bp = b;
     if (b.out_stride == 0) {
         const dim3 grid((uint32_t)ntiles), block(kTile);
-        bp.sub_prefix = bp.tile_sums + ntiles + 1;   // hyobfs_batch_workspace_size
         if (obf)
             hipLaunchKernelGGL(tile_sums_kernel<true>, grid, block, 0, s, bp);
         else

@@ -25,8 +25,8 @@
 
 namespace hyobfs {
 
-// kTileMaxD (kernels.h) datagrams per tile: one wave hashes 16 keys, 4 lanes each;
-// 16 slots of a multiple of 8 bytes are whole 128-byte lines
+constexpr int kTileMaxD = 16;        // datagrams per tile: one wave hashes 16 keys, 4 lanes each;
+                                     // 16 slots of a multiple of 8 bytes are whole 128-byte lines
 constexpr uint64_t kMaxTileSlot = 1u << 20;
 #ifndef HY_TILE_MIN_WAVES
 #define HY_TILE_MIN_WAVES 8
@@ -235,11 +235,7 @@ __device__ __forceinline__ void store16_global(uint8_t* p, uint64_t lo, uint64_t
 
 __device__ __forceinline__ void glds16(const uint8_t* g, uint8_t* l) {   // LDS-DMA: l = wave base + lane * 16
 #ifdef HYOBFS_EMULATE
-    // the device reads whole 16-byte blocks, which never cross a page, so bytes of a
-    // block past the end of an allocation are harmless (and masked off); ASan is told
-    // apart from real overflows by reading only unpoisoned bytes
-    uint8_t* d = l + 16 * (threadIdx.x & 63);
-    for (int i = 0; i < 16; ++i) d[i] = hyemu_readable(g + i) ? g[i] : 0xCD;
+    std::memcpy(l + 16 * (threadIdx.x & 63), g, 16);
 #else
     __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
                                      (__attribute__((address_space(3))) void*)l, 16, 0, HY_TILE_DMA_AUX);

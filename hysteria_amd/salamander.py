@@ -136,7 +136,7 @@ class SalamanderObfuscator:
     def __exit__(self, *exc):
         self.close()
 
-    KERNELS = {"auto": 0, "wave": 1, "tile": 2, "packed": 3}
+    KERNELS = {"auto": 0, "wave": 1, "tile": 2}
 
     def set_kernel(self, kernel: str) -> None:
         """Batch kernel of this context: "auto" (the tile kernel where it applies, else the

@@ -100,15 +100,13 @@ int hyobfs_salamander_device(const hyobfs_salamander* ctx);
    datagrams' payload bytes) -- the uniform 1200-byte batch of the benchmark --
    and the wave-group kernel on every other batch (packed output, ragged
    lengths, any alignment).  HYOBFS_KERNEL_WAVE forces the wave-group kernel;
-   HYOBFS_KERNEL_TILE is AUTO; HYOBFS_KERNEL_PACKED runs packed batches on the
-   pipelined packed kernel (persistent workgroups, tiles of 16 datagrams).  The
-   HYOBFS_KERNEL environment variable (wave|tile|packed) overrides AUTO.  Returns
-   HYOBFS_ERR_INVALID for an unknown value.  Outputs are identical. */
+   HYOBFS_KERNEL_TILE is AUTO.  The HYOBFS_KERNEL environment variable
+   (wave|tile) overrides AUTO.  Returns HYOBFS_ERR_INVALID for an unknown value.
+   Outputs are identical. */
 enum {
     HYOBFS_KERNEL_AUTO = 0,
     HYOBFS_KERNEL_WAVE = 1,
-    HYOBFS_KERNEL_TILE = 2,
-    HYOBFS_KERNEL_PACKED = 3
+    HYOBFS_KERNEL_TILE = 2
 };
 int hyobfs_salamander_set_kernel(hyobfs_salamander* ctx, int kernel);
 
@@ -188,8 +186,6 @@ typedef struct hyobfs_batch {
     uint64_t workspace_bytes;
 } hyobfs_batch;
 
-/* Packed-layout scratch: 8 bytes per 256 datagrams (+8) for the scan's tile
- * sums and 8 bytes per 16 datagrams for the tile offsets inside them. */
 uint64_t hyobfs_batch_workspace_size(uint64_t n);
 int hyobfs_salamander_obfuscate_batch(hyobfs_salamander* ctx, const hyobfs_batch* b,
                                       void* stream);

@@ -29,7 +29,7 @@ def test_abi_basics():
     assert lib.hyobfs_abi_version() == 1
     assert _lib.status_string(_lib.HYOBFS_ERR_PSK_TOO_SHORT) == "PSK must be at least 4 bytes"
     assert lib.hyobfs_batch_workspace_size(0) == 8
-    assert lib.hyobfs_batch_workspace_size(257) == (3 + 17) * 8   # scan tiles + 1, 16-datagram tiles
+    assert lib.hyobfs_batch_workspace_size(257) == 3 * 8
 
 
 def test_psk_too_short_before_device_check():

@@ -35,8 +35,6 @@ def emu_lib():
 # Each test's case: (run_case.py arguments, extra environment), from its parameters.
 SPECS = {
     "test_emulated_packed_auto": lambda p: (p["which"], p["args"], {"HYEMU_CUS": "2"}),
-    "test_emulated_packed_pipelined": lambda p: (p["which"], p["args"], {"HYEMU_CUS": "2",
-                                                                         "HYOBFS_KERNEL": "packed"}),
     "test_emulated_tile_kernel": lambda p: (p["which"], p["args"], {"HYOBFS_KERNEL": "tile", "HYEMU_CUS": "2"}),
     "test_emulated_wave_kernel_forced": lambda p: None if p["which"] in ("conn", "host", "coalesce", "quic",
                                                                          "lifecycle", "deadline") else (
@@ -146,13 +144,6 @@ PACKED_CASES = [
 @pytest.mark.parametrize("which,args", PACKED_CASES)
 def test_emulated_packed_auto(emu_lib, which, args):
     _run(emu_lib, which, args, {"HYEMU_CUS": "2"})
-
-
-# The same cases on the pipelined packed kernel (salamander_packed.h, opt-in): two
-# resident workgroups walk every tile, so each carries several tiles' registers.
-@pytest.mark.parametrize("which,args", PACKED_CASES)
-def test_emulated_packed_pipelined(emu_lib, which, args):
-    _run(emu_lib, which, args, {"HYEMU_CUS": "2", "HYOBFS_KERNEL": "packed"})
 
 
 # The tile kernel (salamander_tile.h): slotted batches whose region edges are all

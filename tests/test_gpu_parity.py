@@ -17,13 +17,12 @@ pytestmark = pytest.mark.gpu
 PSK = b"average_password"
 
 
-@pytest.fixture(scope="module", params=["auto", "wave", "tile", "packed"])
+@pytest.fixture(scope="module", params=["auto", "wave", "tile"])
 def obfs(gpu, request):
     """One context per batch kernel choice: auto (the shipped per-layout choice:
     the tile kernel where it applies, salamander_tile.h, else the wave kernel),
-    the wave-group kernel forced on every layout (salamander_wave.h), tile
-    (= auto, kept as the explicit name) and packed (packed batches on the
-    pipelined packed kernel, salamander_packed.h)."""
+    the wave-group kernel forced on every layout (salamander_wave.h), and tile
+    (= auto, kept as the explicit name)."""
     import hysteria_amd
     o = hysteria_amd.SalamanderObfuscator(PSK, 0)
     o.set_kernel(request.param)
