@@ -249,6 +249,30 @@ __device__ __forceinline__ uint32_t park_index(uint2 ow, uint32_t c) {
     return c == cs ? 0u : (c == cs + 1 && cs + 1 <= ce) ? 1u : (c == ce && ce > cs + 1) ? 2u : 3u;
 }
 
+// Decoupled look-back (one pass, no tile-sum launches): tile t's word is
+// flag (2 bits) | value (62 bits); flag 1 = the tile's own sum, 2 = the inclusive
+// prefix.  Lane 0 publishes the sum, walks back summing own sums until it meets an
+// inclusive prefix, then publishes its own.  Returns the exclusive prefix.
+__device__ __forceinline__ uint64_t tile_lookback(uint64_t* st, uint64_t t, uint64_t tsum, int lane) {
+    constexpr uint64_t kAgg = 1ull << 62, kInc = 2ull << 62, kVal = kAgg - 1;
+    uint64_t excl = 0;
+    if (lane == 0) {
+        if (t == 0) {
+            hy_store_agent(st, kInc | tsum);
+        } else {
+            hy_store_agent(st + t, kAgg | tsum);
+            for (uint64_t u = t - 1;; --u) {
+                uint64_t s;
+                while (((s = hy_load_agent(st + u)) >> 62) == 0) hy_spin_pause();
+                excl += s & kVal;
+                if ((s >> 62) == 2) break;
+            }
+            hy_store_agent(st + t, kInc | (excl + tsum));
+        }
+    }
+    return __shfl(excl, 0, 64);
+}
+
 template <bool OBF, bool PACKED, int SW>
 __global__ __launch_bounds__(kGroup* kWavesPerBlock, HY_WAVE_MIN_WAVES) void
 salamander_wave_kernel(BatchParams B, KeyParams K) {
@@ -257,6 +281,7 @@ salamander_wave_kernel(BatchParams B, KeyParams K) {
     constexpr int U = kWU;
     using GroupBuf = GroupBufT<PACKED>;
     __shared__ GroupBuf gbuf[kWavesPerBlock];
+    __shared__ uint64_t s_scan[kWavesPerBlock + 1];   // packed: group sums, then the tile's prefix
 
     const int lane = threadIdx.x & 63;
     const uint32_t wid = uni32(threadIdx.x >> 6);
@@ -273,7 +298,8 @@ salamander_wave_kernel(BatchParams B, KeyParams K) {
     const uint64_t p = (r << rl) + i;          // this lane's datagram
     const bool live = p < B.n;
     const uint32_t cnt = uni32((uint32_t)wave_sum(live ? 1u : 0u));   // live lanes are a prefix
-    if (cnt == 0) return;
+    // (a wave with no datagram leaves after the packed layout's workgroup barriers)
+    if (cnt == 0 && !(PACKED && RUN == kGroup)) return;
 
     // ---- 1. metadata
     uint32_t L = 0;
@@ -285,12 +311,28 @@ salamander_wave_kernel(BatchParams B, KeyParams K) {
     }
     uint32_t W = live ? out_width<OBF>(L, B.pkt_cap) : 0u;
     uint64_t ooff, rfirst;   // output offset of the datagram / of its run's first datagram
-    if (PACKED && RUN == kGroup) {   // tile prefix + widths of the tile's earlier datagrams + wave scan
-        const uint64_t p0 = w * kGroup;
-        const uint64_t tb = p0 / kTile * kTile;
-        uint32_t pre = 0;
-        for (uint64_t q = tb + lane; q < p0; q += kGroup) pre += out_width<OBF>(pkt_len(B, q), B.pkt_cap);
-        rfirst = uni64(B.tile_prefix[p0 / kTile] + wave_sum(pre));
+    if (PACKED && RUN == kGroup) {
+        // One-pass scan: the workgroup's four groups are one 256-datagram tile; its
+        // width sum is published and the exclusive prefix found by decoupled look-back
+        // over the earlier tiles' words (tile_lookback).  Workgroups start in index
+        // order on every XCD, so the tile a look-back waits for is running or done.
+        static_assert(kGroup * kWavesPerBlock == kTile, "a workgroup is one scan tile");
+        const uint64_t gsum = uni64(wave_sum(W));
+        if (lane == 0) s_scan[wid] = gsum;
+        __syncthreads();
+        uint64_t tsum = 0, wpre = 0;
+#pragma unroll
+        for (uint32_t v = 0; v < (uint32_t)kWavesPerBlock; ++v) {
+            tsum += s_scan[v];
+            wpre += v < wid ? s_scan[v] : 0ull;
+        }
+        if (wid == 0) {
+            const uint64_t tp = tile_lookback(B.tile_status, blockIdx.x, tsum, lane);
+            if (lane == 0) s_scan[kWavesPerBlock] = tp;
+        }
+        __syncthreads();
+        if (cnt == 0) return;
+        rfirst = uni64(s_scan[kWavesPerBlock] + wpre);
         ooff = rfirst + wave_incl_scan(W, lane) - W;
     } else if (PACKED) {   // shorter runs: the same per run, over the run's RUN lanes
         const uint64_t s0 = r << rl;   // the run's first datagram
