@@ -196,8 +196,8 @@ hipError_t launch_salamander(bool obf, const BatchParams& b, const KeyParams& k,
         if (wave_packed_run_log2() == 6) {
             // runs of 64: the wave kernel scans in the same launch (decoupled look-back,
             // salamander_wave.h tile_lookback) over per-tile words zeroed here
-            bp.tile_status = bp.tile_sums;
-            const hipError_t e = hipMemsetAsync(bp.tile_status, 0, ntiles * sizeof(uint64_t), s);
+            bp.tile_status = bp.tile_sums;   // ntiles words, then the tile counter
+            const hipError_t e = hipMemsetAsync(bp.tile_status, 0, (ntiles + 1) * sizeof(uint64_t), s);
             if (e != hipSuccess) return e;
         } else {   // shorter runs: tile sums and their exclusive scan first
             const dim3 grid((uint32_t)ntiles), block(kTile);

@@ -249,7 +249,8 @@ __device__ __forceinline__ uint32_t park_index(uint2 ow, uint32_t c) {
     return c == cs ? 0u : (c == cs + 1 && cs + 1 <= ce) ? 1u : (c == ce && ce > cs + 1) ? 2u : 3u;
 }
 
-// Decoupled look-back (one pass, no tile-sum launches): tile t's word is
+// Decoupled look-back (one pass, no tile-sum launches; tiles taken in start
+// order, see the kernel): tile t's word is
 // flag (2 bits) | value (62 bits); flag 1 = the tile's own sum, 2 = the inclusive
 // prefix.  Lane 0 publishes the sum, walks back summing own sums until it meets an
 // inclusive prefix, then publishes its own.  Returns the exclusive prefix.
@@ -281,7 +282,7 @@ salamander_wave_kernel(BatchParams B, KeyParams K) {
     constexpr int U = kWU;
     using GroupBuf = GroupBufT<PACKED>;
     __shared__ GroupBuf gbuf[kWavesPerBlock];
-    __shared__ uint64_t s_scan[kWavesPerBlock + 1];   // packed: group sums, then the tile's prefix
+    __shared__ uint64_t s_scan[kWavesPerBlock + 2];   // packed: group sums, the tile's prefix, its index
 
     const int lane = threadIdx.x & 63;
     const uint32_t wid = uni32(threadIdx.x >> 6);
@@ -292,7 +293,18 @@ salamander_wave_kernel(BatchParams B, KeyParams K) {
     // on neighbouring runs and the chip sweeps memory in address order.
     const uint32_t rl = B.run_log2, RUN = 1u << rl;
     const uint64_t Wt = (uint64_t)gridDim.x * kWavesPerBlock;
-    const uint64_t w = (uint64_t)blockIdx.x * kWavesPerBlock + wid;
+    // Packed runs of 64: the workgroup's tile is taken in start order from a
+    // counter (B.tile_status[gridDim.x]), so every tile its look-back waits for
+    // was taken earlier by a workgroup that is running or done, whatever the
+    // dispatch order (which HIP leaves undefined).
+    uint64_t blk = blockIdx.x;
+    if (PACKED && RUN == kGroup) {
+        if (threadIdx.x == 0)
+            s_scan[kWavesPerBlock + 1] = atomicAdd((unsigned long long*)(B.tile_status + gridDim.x), 1ull);
+        __syncthreads();
+        blk = uni64(s_scan[kWavesPerBlock + 1]);
+    }
+    const uint64_t w = blk * kWavesPerBlock + wid;
     const uint32_t j = (uint32_t)lane >> rl, i = (uint32_t)lane & (RUN - 1);
     const uint64_t r = (uint64_t)j * Wt + w;   // this lane's run
     const uint64_t p = (r << rl) + i;          // this lane's datagram
@@ -327,7 +339,7 @@ salamander_wave_kernel(BatchParams B, KeyParams K) {
             wpre += v < wid ? s_scan[v] : 0ull;
         }
         if (wid == 0) {
-            const uint64_t tp = tile_lookback(B.tile_status, blockIdx.x, tsum, lane);
+            const uint64_t tp = tile_lookback(B.tile_status, blk, tsum, lane);
             if (lane == 0) s_scan[kWavesPerBlock] = tp;
         }
         __syncthreads();
