@@ -39,7 +39,10 @@ constexpr int kWU = HY_WU;           // chunks per lane per sweep iteration
 #define HY_RUN_LOG2 3
 #endif
 #ifndef HY_WAVE_MIN_WAVES
-#define HY_WAVE_MIN_WAVES 8          // __launch_bounds__ min waves per SIMD
+#define HY_WAVE_MIN_WAVES 8          // __launch_bounds__ min waves per SIMD (slotted layout)
+#endif
+#ifndef HY_PACKED_MIN_WAVES
+#define HY_PACKED_MIN_WAVES 7        // packed layout: its LDS (128 park slots, 23 KB per workgroup) fits 7
 #endif
 
 #ifndef HY_PACKED_PARK_SLOTS
@@ -275,7 +278,7 @@ __device__ __forceinline__ uint64_t tile_lookback(uint64_t* st, uint64_t t, uint
 }
 
 template <bool OBF, bool PACKED, int SW>
-__global__ __launch_bounds__(kGroup* kWavesPerBlock, HY_WAVE_MIN_WAVES) void
+__global__ __launch_bounds__(kGroup* kWavesPerBlock, PACKED ? HY_PACKED_MIN_WAVES : HY_WAVE_MIN_WAVES) void
 salamander_wave_kernel(BatchParams B, KeyParams K) {
     constexpr uint32_t SALT = OBF ? 8u : 0u;   // salt bytes in front of the output payload
     constexpr uint32_t SKIP = OBF ? 0u : 8u;   // salt bytes in front of the input payload
