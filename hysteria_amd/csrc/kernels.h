@@ -28,23 +28,6 @@ __device__ __forceinline__ void hy_wave_sync() {
 }
 #endif
 
-// 64-bit words shared between workgroups of one launch (the packed layout's
-// look-back scan): relaxed atomics at agent scope, so every XCD sees them
-// (vector memory instructions; nothing goes through the scalar cache).
-#ifdef HYOBFS_EMULATE
-inline uint64_t hy_load_agent(const uint64_t* p) { return __atomic_load_n(p, __ATOMIC_ACQUIRE); }
-inline void hy_store_agent(uint64_t* p, uint64_t v) { __atomic_store_n(p, v, __ATOMIC_RELEASE); }
-inline void hy_spin_pause() { std::this_thread::yield(); }
-#else
-__device__ __forceinline__ uint64_t hy_load_agent(const uint64_t* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void hy_store_agent(uint64_t* p, uint64_t v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void hy_spin_pause() { __builtin_amdgcn_s_sleep(2); }
-#endif
-
 constexpr int kTile = 256;          // datagrams per tile-sum entry of the packed layout's scan
 constexpr uint32_t kMaxDatagram = (1u << 24) - 64;  // longest datagram a batch accepts
 constexpr uint64_t kMaxStride = 1ull << 24;         // longest slot of a slotted output
@@ -81,7 +64,6 @@ struct BatchParams {
     unsigned long long* out_total;
     const uint64_t* tile_prefix;  // packed: exclusive prefix of tile sums (ntiles+1)
     uint64_t* tile_sums;          // packed: scratch, ntiles+1 entries
-    uint64_t* tile_status;        // packed, runs of 64: look-back words per tile (zeroed per launch)
     uint32_t run_log2;            // wave kernel: datagrams per run = 2^run_log2
     int kernel;                   // HYOBFS_KERNEL_* of the context (0 = auto)
 };

@@ -193,21 +193,13 @@ hipError_t launch_salamander(bool obf, const BatchParams& b, const KeyParams& k,
     if (k.nblk == 2 && (k.salt_pos >> 3) != 15) return hipErrorInvalidValue;   // by construction
     BatchParams bp = b;
     if (b.out_stride == 0) {
-        if (wave_packed_run_log2() == 6) {
-            // runs of 64: the wave kernel scans in the same launch (decoupled look-back,
-            // salamander_wave.h tile_lookback) over per-tile words zeroed here
-            bp.tile_status = bp.tile_sums;   // ntiles words, then the tile counter
-            const hipError_t e = hipMemsetAsync(bp.tile_status, 0, (ntiles + 1) * sizeof(uint64_t), s);
-            if (e != hipSuccess) return e;
-        } else {   // shorter runs: tile sums and their exclusive scan first
-            const dim3 grid((uint32_t)ntiles), block(kTile);
-            if (obf)
-                hipLaunchKernelGGL(tile_sums_kernel<true>, grid, block, 0, s, bp);
-            else
-                hipLaunchKernelGGL(tile_sums_kernel<false>, grid, block, 0, s, bp);
-            hipLaunchKernelGGL(scan_tiles_kernel, dim3(1), dim3(1024), 0, s, bp.tile_sums, ntiles);
-            bp.tile_prefix = bp.tile_sums;
-        }
+        const dim3 grid((uint32_t)ntiles), block(kTile);
+        if (obf)
+            hipLaunchKernelGGL(tile_sums_kernel<true>, grid, block, 0, s, bp);
+        else
+            hipLaunchKernelGGL(tile_sums_kernel<false>, grid, block, 0, s, bp);
+        hipLaunchKernelGGL(scan_tiles_kernel, dim3(1), dim3(1024), 0, s, bp.tile_sums, ntiles);
+        bp.tile_prefix = bp.tile_sums;
         if (obf)
             launch_main<true, true>(bp, k, s);
         else

@@ -252,31 +252,6 @@ __device__ __forceinline__ uint32_t park_index(uint2 ow, uint32_t c) {
     return c == cs ? 0u : (c == cs + 1 && cs + 1 <= ce) ? 1u : (c == ce && ce > cs + 1) ? 2u : 3u;
 }
 
-// Decoupled look-back (one pass, no tile-sum launches; tiles taken in start
-// order, see the kernel): tile t's word is
-// flag (2 bits) | value (62 bits); flag 1 = the tile's own sum, 2 = the inclusive
-// prefix.  Lane 0 publishes the sum, walks back summing own sums until it meets an
-// inclusive prefix, then publishes its own.  Returns the exclusive prefix.
-__device__ __forceinline__ uint64_t tile_lookback(uint64_t* st, uint64_t t, uint64_t tsum, int lane) {
-    constexpr uint64_t kAgg = 1ull << 62, kInc = 2ull << 62, kVal = kAgg - 1;
-    uint64_t excl = 0;
-    if (lane == 0) {
-        if (t == 0) {
-            hy_store_agent(st, kInc | tsum);
-        } else {
-            hy_store_agent(st + t, kAgg | tsum);
-            for (uint64_t u = t - 1;; --u) {
-                uint64_t s;
-                while (((s = hy_load_agent(st + u)) >> 62) == 0) hy_spin_pause();
-                excl += s & kVal;
-                if ((s >> 62) == 2) break;
-            }
-            hy_store_agent(st + t, kInc | (excl + tsum));
-        }
-    }
-    return __shfl(excl, 0, 64);
-}
-
 template <bool OBF, bool PACKED, int SW>
 __global__ __launch_bounds__(kGroup* kWavesPerBlock, PACKED ? HY_PACKED_MIN_WAVES : HY_WAVE_MIN_WAVES) void
 salamander_wave_kernel(BatchParams B, KeyParams K) {
@@ -285,7 +260,6 @@ salamander_wave_kernel(BatchParams B, KeyParams K) {
     constexpr int U = kWU;
     using GroupBuf = GroupBufT<PACKED>;
     __shared__ GroupBuf gbuf[kWavesPerBlock];
-    __shared__ uint64_t s_scan[kWavesPerBlock + 2];   // packed: group sums, the tile's prefix, its index
 
     const int lane = threadIdx.x & 63;
     const uint32_t wid = uni32(threadIdx.x >> 6);
@@ -296,25 +270,13 @@ salamander_wave_kernel(BatchParams B, KeyParams K) {
     // on neighbouring runs and the chip sweeps memory in address order.
     const uint32_t rl = B.run_log2, RUN = 1u << rl;
     const uint64_t Wt = (uint64_t)gridDim.x * kWavesPerBlock;
-    // Packed runs of 64: the workgroup's tile is taken in start order from a
-    // counter (B.tile_status[gridDim.x]), so every tile its look-back waits for
-    // was taken earlier by a workgroup that is running or done, whatever the
-    // dispatch order (which HIP leaves undefined).
-    uint64_t blk = blockIdx.x;
-    if (PACKED && RUN == kGroup) {
-        if (threadIdx.x == 0)
-            s_scan[kWavesPerBlock + 1] = atomicAdd((unsigned long long*)(B.tile_status + gridDim.x), 1ull);
-        __syncthreads();
-        blk = uni64(s_scan[kWavesPerBlock + 1]);
-    }
-    const uint64_t w = blk * kWavesPerBlock + wid;
+    const uint64_t w = (uint64_t)blockIdx.x * kWavesPerBlock + wid;
     const uint32_t j = (uint32_t)lane >> rl, i = (uint32_t)lane & (RUN - 1);
     const uint64_t r = (uint64_t)j * Wt + w;   // this lane's run
     const uint64_t p = (r << rl) + i;          // this lane's datagram
     const bool live = p < B.n;
     const uint32_t cnt = uni32((uint32_t)wave_sum(live ? 1u : 0u));   // live lanes are a prefix
-    // (a wave with no datagram leaves after the packed layout's workgroup barriers)
-    if (cnt == 0 && !(PACKED && RUN == kGroup)) return;
+    if (cnt == 0) return;
 
     // ---- 1. metadata
     uint32_t L = 0;
@@ -326,28 +288,12 @@ salamander_wave_kernel(BatchParams B, KeyParams K) {
     }
     uint32_t W = live ? out_width<OBF>(L, B.pkt_cap) : 0u;
     uint64_t ooff, rfirst;   // output offset of the datagram / of its run's first datagram
-    if (PACKED && RUN == kGroup) {
-        // One-pass scan: the workgroup's four groups are one 256-datagram tile; its
-        // width sum is published and the exclusive prefix found by decoupled look-back
-        // over the earlier tiles' words (tile_lookback).  Workgroups start in index
-        // order on every XCD, so the tile a look-back waits for is running or done.
-        static_assert(kGroup * kWavesPerBlock == kTile, "a workgroup is one scan tile");
-        const uint64_t gsum = uni64(wave_sum(W));
-        if (lane == 0) s_scan[wid] = gsum;
-        __syncthreads();
-        uint64_t tsum = 0, wpre = 0;
-#pragma unroll
-        for (uint32_t v = 0; v < (uint32_t)kWavesPerBlock; ++v) {
-            tsum += s_scan[v];
-            wpre += v < wid ? s_scan[v] : 0ull;
-        }
-        if (wid == 0) {
-            const uint64_t tp = tile_lookback(B.tile_status, blk, tsum, lane);
-            if (lane == 0) s_scan[kWavesPerBlock] = tp;
-        }
-        __syncthreads();
-        if (cnt == 0) return;
-        rfirst = uni64(s_scan[kWavesPerBlock] + wpre);
+    if (PACKED && RUN == kGroup) {   // tile prefix + widths of the tile's earlier datagrams + wave scan
+        const uint64_t p0 = w * kGroup;
+        const uint64_t tb = p0 / kTile * kTile;
+        uint32_t pre = 0;
+        for (uint64_t q = tb + lane; q < p0; q += kGroup) pre += out_width<OBF>(pkt_len(B, q), B.pkt_cap);
+        rfirst = uni64(B.tile_prefix[p0 / kTile] + wave_sum(pre));
         ooff = rfirst + wave_incl_scan(W, lane) - W;
     } else if (PACKED) {   // shorter runs: the same per run, over the run's RUN lanes
         const uint64_t s0 = r << rl;   // the run's first datagram
