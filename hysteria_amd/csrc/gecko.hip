@@ -261,33 +261,48 @@ __device__ __forceinline__ void gecko_encode_aligned(const KeyParams& K, const h
             else if (cov) store_masked(ob + a, r, cov);
         }
     }
-    // ---- sweep: lane windows move forward by 64 chunks, so the frame walk does too
+    // ---- sweep: lane windows move forward by 64 chunks, so the frame walk does too.
+    // Per iteration: every lane issues its kGkU loads unconditionally (a chunk that
+    // is not message bytes reads the 16-byte hy_safe_line), then the padding chunks
+    // are computed and stored, then the message chunks.  With the loads under a
+    // branch the compiler waited for vmcnt(0) before every store, i.e. for the
+    // previous store's completion; this way each message store waits only for its
+    // own load, and the keystream work runs while the loads are in flight.
     uint32_t q = 0;
     for (uint32_t T = 0; T < tc; T += 64 * kGkU) {
         gk_u128 v[kGkU];
-        bool ok[kGkU];
+        uint32_t kq[kGkU];
+        uint8_t kind[kGkU];   // 0 nothing, 1 padding, 2 message bytes
 #pragma unroll
         for (int u = 0; u < kGkU; ++u) {
             const uint32_t c = T + lane + 64 * u, a = 16 * c;
-            v[u] = 0;
-            ok[u] = false;
-            bool pad = false;
+            kind[u] = 0;
+            const uint8_t* src = hy_safe_line();
             if (c < tc) {
                 while (G.rs[q + 1] <= a) ++q;   // rs[64] = the range end > a stops it
                 int32_t p, hp;
-                ok[u] = interior(q, a, p, hp);
-                pad = ok[u] && p < hp;
-                if (ok[u] && !pad) v[u] = gk_load16u(B.msg + G.chunk_off[q] + (p - hp));
+                if (interior(q, a, p, hp)) {
+                    kind[u] = p < hp ? 1 : 2;
+                    if (p >= hp) src = B.msg + G.chunk_off[q] + (p - hp);
+                }
             }
-            if (__ballot(pad)) {   // the whole wave: a quad computes one 64-byte block
-                const gk_u128 ks = gk_ks_quad(P, (uint32_t)((base + 16ull * c) >> 6), lane & 3u);
-                if (pad) v[u] = ks;
-            }
-            if (ok[u]) v[u] ^= G.key[2 * q + ((a >> 4) & 1)];
+            kq[u] = q;
+            v[u] = gk_load16u(src);
         }
 #pragma unroll
-        for (int u = 0; u < kGkU; ++u)
-            if (ok[u]) store16_stream(ob + 16 * (T + lane + 64 * u), v[u]);
+        for (int u = 0; u < kGkU; ++u) {
+            const bool pad = kind[u] == 1;
+            if (__ballot(pad)) {   // the whole wave: a quad computes one 64-byte block
+                const uint32_t c = T + lane + 64 * u;
+                const gk_u128 ks = gk_ks_quad(P, (uint32_t)((base + 16ull * c) >> 6), lane & 3u);
+                if (pad) store16_stream(ob + 16 * c, ks ^ G.key[2 * kq[u] + (c & 1)]);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < kGkU; ++u) {
+            const uint32_t c = T + lane + 64 * u;
+            if (kind[u] == 2) store16_stream(ob + 16 * c, v[u] ^ G.key[2 * kq[u] + (c & 1)]);
+        }
     }
 }
 

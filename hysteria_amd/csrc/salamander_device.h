@@ -165,6 +165,18 @@ __device__ __forceinline__ uint32_t out_width(uint32_t L, uint32_t cap) {
     }
 }
 
+// 16 readable bytes for loads whose value is discarded (sweeps that issue their
+// loads unconditionally, so the compiler's vmcnt waits stay exact)
+__device__ __forceinline__ const uint8_t* hy_safe_line() {
+#ifdef HYOBFS_EMULATE
+    static const uint8_t z[64] = {};
+    return z;
+#else
+    static __device__ uint8_t z[64];
+    return z;
+#endif
+}
+
 __device__ __forceinline__ uint32_t pkt_len(const BatchParams& B, uint64_t p) {
     return B.in_len ? B.in_len[p] : B.len_uniform;
 }
