@@ -24,7 +24,7 @@ K = int(os.environ.get("AB_STEPS", "10"))
 R = int(os.environ.get("AB_ROUNDS", "6"))
 libs = [kv.split("=", 1) for kv in os.environ.get("AB_LIBS", "main=" + hysteria_amd._lib.LIB_PATH).split(",")]
 dev = torch.device("cuda:0")
-M, L = 262144, 1200
+M, L = int(os.environ.get("AB_MSGS", "262144")), 1200
 rng = np.random.default_rng(1)
 fr, off, total = gecko.plan_fragments(np.full(M, L), rand32=lambda k: rng.integers(0, 2**32, k, dtype=np.uint64))
 nf = len(fr)
