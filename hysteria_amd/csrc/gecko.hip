@@ -38,6 +38,9 @@ __device__ __forceinline__ gk_u128 gk_mask(uint32_t lo, uint32_t hi) {   // byte
     return m << (8 * lo);
 }
 
+#ifndef HY_GK_PIPE
+#define HY_GK_PIPE 1   // software-pipelined aligned sweep (two iterations' loads in flight)
+#endif
 #ifndef HY_GK_U
 #define HY_GK_U 4
 #endif
@@ -234,7 +237,11 @@ __device__ __forceinline__ void gecko_encode_aligned(const KeyParams& K, const h
     // still in the L2 when the sweep's streaming stores complete it): the first two (salt, header), the one holding
     // the padding/chunk seam, the last; a chunk an earlier frame reaches into is that
     // frame's, and its owner merges every frame that touches it
+#ifdef HY_X_NOEDGE   // ablation builds only (timing experiments; wrong output)
+    if (false) {
+#else
     if (valid) {
+#endif
         const uint32_t hp = G.hp_plain[lane] & 0xffff;
         const uint32_t cs = rs >> 4, ce = (rs + HYOBFS_SALT_LEN + plain - 1) >> 4;
         const uint32_t seam = (rs + HYOBFS_SALT_LEN + hp - 1) >> 4;
@@ -268,50 +275,83 @@ __device__ __forceinline__ void gecko_encode_aligned(const KeyParams& K, const h
     // branch the compiler waited for vmcnt(0) before every store, i.e. for the
     // previous store's completion; this way each message store waits only for its
     // own load, and the keystream work runs while the loads are in flight.
-    uint32_t q = 0;
-    for (uint32_t T = 0; T < tc; T += 64 * kGkU) {
+    struct Step {   // one iteration: kGkU chunks per lane
         gk_u128 v[kGkU];
         uint32_t kq[kGkU];
         uint8_t kind[kGkU];   // 0 nothing, 1 padding, 2 message bytes
+    };
+    uint32_t q = 0;
+    auto issue = [&](uint32_t T, Step& S) {
 #pragma unroll
         for (int u = 0; u < kGkU; ++u) {
             const uint32_t c = T + lane + 64 * u, a = 16 * c;
-            kind[u] = 0;
+            S.kind[u] = 0;
             const uint8_t* src = hy_safe_line();
             if (c < tc) {
                 while (G.rs[q + 1] <= a) ++q;   // rs[64] = the range end > a stops it
                 int32_t p, hp;
                 if (interior(q, a, p, hp)) {
-                    kind[u] = p < hp ? 1 : 2;
+                    S.kind[u] = p < hp ? 1 : 2;
                     if (p >= hp) src = B.msg + G.chunk_off[q] + (p - hp);
                 }
             }
-            kq[u] = q;
-            v[u] = gk_load16u(src);
+            S.kq[u] = q;
+            S.v[u] = gk_load16u(src);
         }
+    };
+    auto retire = [&](uint32_t T, const Step& S) {
 #pragma unroll
         for (int u = 0; u < kGkU; ++u) {
-            const bool pad = kind[u] == 1;
+            const bool pad = S.kind[u] == 1;
             if (__ballot(pad)) {   // the whole wave: a quad computes one 64-byte block
                 const uint32_t c = T + lane + 64 * u;
+#ifdef HY_X_NOKS   // ablation builds only (timing experiments; wrong output)
+                const gk_u128 ks = (gk_u128)(base + 16ull * c);
+#else
                 const gk_u128 ks = gk_ks_quad(P, (uint32_t)((base + 16ull * c) >> 6), lane & 3u);
-                if (pad) store16_stream(ob + 16 * c, ks ^ G.key[2 * kq[u] + (c & 1)]);
+#endif
+                if (pad) store16_stream(ob + 16 * c, ks ^ G.key[2 * S.kq[u] + (c & 1)]);
             }
         }
 #pragma unroll
         for (int u = 0; u < kGkU; ++u) {
             const uint32_t c = T + lane + 64 * u;
-            if (kind[u] == 2) store16_stream(ob + 16 * c, v[u] ^ G.key[2 * kq[u] + (c & 1)]);
+            if (S.kind[u] == 2) store16_stream(ob + 16 * c, S.v[u] ^ G.key[2 * S.kq[u] + (c & 1)]);
+        }
+    };
+    constexpr uint32_t STEP = 64 * kGkU;
+#if HY_GK_PIPE
+    // Software pipelined: iteration i+1's loads are issued before iteration i's
+    // stores, so waiting for them never waits for those stores (vmcnt counts loads
+    // and stores in issue order); past the range end issue() reads only the safe line.
+    {
+        Step S0, S1;
+        issue(0, S0);
+        for (uint32_t T = 0; T < tc; T += 2 * STEP) {
+            issue(T + STEP, S1);
+            retire(T, S0);
+            if (T + STEP >= tc) break;
+            issue(T + 2 * STEP, S0);
+            retire(T + STEP, S1);
         }
     }
+#else
+    for (uint32_t T = 0; T < tc; T += STEP) {
+        Step S;
+        issue(T, S);
+        retire(T, S);
+    }
+#endif
 }
 
-// Register cap: 6 waves/SIMD (80 VGPRs, a few spilled around the hash) measured fastest
-// with the per-salt-word key: 0.561 ms against 0.567 at 5 waves (94 VGPRs), 0.623 for the
+// Register cap: 5 waves/SIMD with the pipelined sweep (two iterations' registers):
+// 0.536-0.539 ms against 0.545 at 6 waves and 0.551 unpipelined at 6
+// (profiles/r03_ab_gecko_pipe.txt).  Unpipelined, 6 waves measured fastest with the
+// per-salt-word key: 0.561 ms against 0.567 at 5 waves (94 VGPRs), 0.623 for the
 // generic key at 4 waves (97 VGPRs) and 0.734 at 8 waves (heavy spills),
 // profiles/r03_ab_gecko_occupancy.txt.
 #ifndef HY_GK_WPE
-#define HY_GK_WPE 6
+#define HY_GK_WPE 5
 #endif
 #ifdef HYOBFS_EMULATE
 #define HY_GK_ATTR
@@ -350,7 +390,11 @@ __global__ __launch_bounds__(256) HY_GK_ATTR void gecko_encode_kernel(KeyParams 
             salt = B.salts[f];
             // keyLocked (salamander.go:88-91) in registers; the hash overlaps other waves' sweeps
             uint64_t kw[4];
+#ifdef HY_X_NOGKHASH   // ablation builds only (timing experiments; wrong output)
+            kw[0] = salt; kw[1] = salt * 3; kw[2] = salt ^ 7; kw[3] = salt + 1;
+#else
             wave_key<SW>(K, salt, kw);
+#endif
             k0 = (gk_u128)kw[1] << 64 | kw[0];
             k1 = (gk_u128)kw[3] << 64 | kw[2];
         }
