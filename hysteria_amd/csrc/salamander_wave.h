@@ -42,13 +42,20 @@ constexpr int kWU = HY_WU;           // chunks per lane per sweep iteration
 #define HY_WAVE_MIN_WAVES 8          // __launch_bounds__ min waves per SIMD (slotted layout)
 #endif
 #ifndef HY_PACKED_MIN_WAVES
-#define HY_PACKED_MIN_WAVES 7        // packed layout: its LDS (128 park slots, 23 KB per workgroup) fits 7
+#define HY_PACKED_MIN_WAVES (HY_PACKED_PARK_SLOTS > 64 ? 7 : 8)   // what the packed LDS (park slots) allows
 #endif
 
+#ifndef HY_PACKED_DPW
+#define HY_PACKED_DPW 32             // packed runs of 64: datagrams per wave (lanes 0..DPW-1 own one)
+#endif
 #ifndef HY_PACKED_PARK_SLOTS
-#define HY_PACKED_PARK_SLOTS 128     // park slots per group, packed layout: ragged mixes have up to ~2
-                                     // boundary chunks per datagram (64 slots overflowed into byte-masked
-                                     // late stores; profiles/r02_ab_packed_park_slots.txt)
+#define HY_PACKED_PARK_SLOTS 64      // park slots per group, packed layout: ragged mixes have up to ~2
+                                     // boundary chunks per datagram, so 64 slots fit 32 datagrams per wave
+                                     // (with 64 per wave they overflowed into byte-masked late stores and
+                                     // 128 slots were needed, profiles/r02_ab_packed_park_slots.txt).
+                                     // 32 per wave + 64 slots (4736 B of LDS per wave: 8 waves/SIMD) ran
+                                     // 0.8-1.0 % faster than 64 + 128 (7 waves), 16 per wave 28 % slower
+                                     // (profiles/r03_ab_packed_dpw.txt)
 #endif
 template <bool PACKED>
 struct GroupBufT {                   // one wave's group, in LDS (4736 B with 64 slots: 8 workgroups per CU)
@@ -273,8 +280,11 @@ salamander_wave_kernel(BatchParams B, KeyParams K) {
     const uint64_t w = (uint64_t)blockIdx.x * kWavesPerBlock + wid;
     const uint32_t j = (uint32_t)lane >> rl, i = (uint32_t)lane & (RUN - 1);
     const uint64_t r = (uint64_t)j * Wt + w;   // this lane's run
-    const uint64_t p = (r << rl) + i;          // this lane's datagram
-    const bool live = p < B.n;
+    // packed runs of 64: a wave takes DPW consecutive datagrams (lanes 0..DPW-1)
+    constexpr uint32_t DPW = PACKED ? HY_PACKED_DPW : kGroup;
+    const bool one_run = PACKED && RUN == kGroup;
+    const uint64_t p = one_run ? w * DPW + (uint64_t)lane : (r << rl) + i;   // this lane's datagram
+    const bool live = p < B.n && (!one_run || (uint32_t)lane < DPW);
     const uint32_t cnt = uni32((uint32_t)wave_sum(live ? 1u : 0u));   // live lanes are a prefix
     if (cnt == 0) return;
 
@@ -289,7 +299,7 @@ salamander_wave_kernel(BatchParams B, KeyParams K) {
     uint32_t W = live ? out_width<OBF>(L, B.pkt_cap) : 0u;
     uint64_t ooff, rfirst;   // output offset of the datagram / of its run's first datagram
     if (PACKED && RUN == kGroup) {   // tile prefix + widths of the tile's earlier datagrams + wave scan
-        const uint64_t p0 = w * kGroup;
+        const uint64_t p0 = w * DPW;
         const uint64_t tb = p0 / kTile * kTile;
         uint32_t pre = 0;
         for (uint64_t q = tb + lane; q < p0; q += kGroup) pre += out_width<OBF>(pkt_len(B, q), B.pkt_cap);
@@ -489,7 +499,7 @@ salamander_wave_kernel(BatchParams B, KeyParams K) {
         const uint32_t cand[3] = {cs, cs + 1, ce};
         uint8_t* outb = B.out + G.delta[lane];   // a chunk's contributors share its run
         auto salt_of = [&](uint32_t k) {   // datagram index of lane k: its run, then its place in the run
-            return B.salts[((((uint64_t)(k >> rl)) * Wt + w) << rl) + (k & (RUN - 1))];
+            return B.salts[one_run ? w * DPW + k : ((((uint64_t)(k >> rl)) * Wt + w) << rl) + (k & (RUN - 1))];
         };
 #pragma unroll
         for (int t = 0; t < 3; ++t) {
@@ -532,10 +542,10 @@ inline uint32_t wave_run_log2() {
 
 template <bool OBF, bool PACKED, int SW>
 void launch_wave_sw(const BatchParams& bp, const KeyParams& k, hipStream_t s) {
-    const uint64_t ngroups = div_up(bp.n, kGroup);
-    const uint64_t blocks = div_up(ngroups, kWavesPerBlock);
     BatchParams b = bp;
     b.run_log2 = PACKED ? wave_packed_run_log2() : wave_run_log2();
+    const uint64_t ngroups = div_up(bp.n, PACKED && b.run_log2 == 6 ? (uint64_t)HY_PACKED_DPW : (uint64_t)kGroup);
+    const uint64_t blocks = div_up(ngroups, kWavesPerBlock);
     hipLaunchKernelGGL((salamander_wave_kernel<OBF, PACKED, SW>), dim3((uint32_t)blocks),
                        dim3(kGroup * kWavesPerBlock), 0, s, b, k);
 }
