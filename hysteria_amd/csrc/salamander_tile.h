@@ -37,6 +37,7 @@ struct TileParams {
     uint32_t W;      // output width, a multiple of 8, 16 <= W <= S
     uint32_t LI;     // input bytes per datagram (len_uniform)
     float invS;      // 1 / S
+    uint64_t t0;     // first tile of this launch (launch_tile_sw splits big batches)
 };
 
 #ifndef HY_TILE_SU
@@ -259,7 +260,7 @@ __global__ __launch_bounds__(256, HY_TILE_MIN_WAVES) void salamander_tile_kernel
     const uint32_t tid = threadIdx.x, lane = tid & 63;
     const uint32_t wid = uni32(tid >> 6);
     const uint32_t S = T.S, W = T.W;
-    const uint64_t p0 = (uint64_t)blockIdx.x * kTileMaxD;
+    const uint64_t p0 = (T.t0 + blockIdx.x) * kTileMaxD;
     const uint32_t nt = (uint32_t)min<uint64_t>((uint64_t)kTileMaxD, B.n - p0);
     const uint32_t tbytes = (nt - 1) * S + W;   // tile-local end of the last region
     const uint8_t* __restrict__ ib = B.in + p0 * B.in_stride;
@@ -375,16 +376,41 @@ inline bool tile_params(const BatchParams& b, TileParams& T) {
     T.W = (uint32_t)W;
     T.LI = (uint32_t)L;
     T.invS = 1.0f / (float)S;
+    T.t0 = 0;
     return true;
+}
+
+// Tiles per launch: a big batch goes out as consecutive launches of at most this
+// many tiles (HYOBFS_TILE_LAUNCH_TILES overrides; 0 = one launch).  On an 8M x 1200 B
+// batch one launch ran at 72.6 % of 8 TB/s and eight launches of 1M at 75.4 %
+// (profiles/r03_size_probe.txt): within one long launch the XCDs drift apart in the
+// address space, every launch boundary lines them up again.
+#ifndef HY_TILE_LAUNCH_TILES
+#define HY_TILE_LAUNCH_TILES 65536   // 1M datagrams
+#endif
+inline uint64_t tile_launch_tiles() {
+    static long long v = -1;
+    if (v < 0) {
+        const char* e = std::getenv("HYOBFS_TILE_LAUNCH_TILES");
+        v = e ? std::atoll(e) : HY_TILE_LAUNCH_TILES;
+        if (v < 0) v = 0;
+    }
+    return (uint64_t)v;
 }
 
 template <bool OBF, int SW>
 void launch_tile_sw(const BatchParams& b, const KeyParams& k, const TileParams& T, hipStream_t s) {
-    const uint64_t blocks = div_up(b.n, kTileMaxD);
+    const uint64_t tiles = div_up(b.n, kTileMaxD);
+    const uint64_t per = tile_launch_tiles() ? tile_launch_tiles() : tiles;
     // dynamic LDS: the longest tile input range, 15 strides plus one datagram (in_stride may be
     // smaller than the length, e.g. 0 for one datagram)
     const uint32_t shm = (uint32_t)(((kTileMaxD - 1) * b.in_stride + T.LI + 15) & ~15ull);
-    hipLaunchKernelGGL((salamander_tile_kernel<OBF, SW>), dim3((uint32_t)blocks), dim3(256), shm, s, b, k, T);
+    for (uint64_t t0 = 0; t0 < tiles; t0 += per) {
+        TileParams Tl = T;
+        Tl.t0 = t0;
+        const uint64_t blocks = min(per, tiles - t0);
+        hipLaunchKernelGGL((salamander_tile_kernel<OBF, SW>), dim3((uint32_t)blocks), dim3(256), shm, s, b, k, Tl);
+    }
 }
 
 }  // namespace hyobfs
