@@ -382,11 +382,13 @@ inline bool tile_params(const BatchParams& b, TileParams& T) {
 
 // Tiles per launch: a big batch goes out as consecutive launches of at most this
 // many tiles (HYOBFS_TILE_LAUNCH_TILES overrides; 0 = one launch).  On an 8M x 1200 B
-// batch one launch ran at 72.6 % of 8 TB/s and eight launches of 1M at 75.4 %
+// batch one launch ran at 70.5-72.6 % of 8 TB/s and launches of 1M at 75.4-76.8 %
 // (profiles/r03_size_probe.txt): within one long launch the XCDs drift apart in the
-// address space, every launch boundary lines them up again.
+// address space, every launch boundary lines them up again.  Launches of 512K
+// datagrams ran best on 1M and 8M batches in both directions (78.2-78.4 % obfuscate;
+// 256K 77.5-77.7 %, 1M 77.3-77.6 %, 128K 74.5-74.7 %: launch gaps).
 #ifndef HY_TILE_LAUNCH_TILES
-#define HY_TILE_LAUNCH_TILES 65536   // 1M datagrams
+#define HY_TILE_LAUNCH_TILES 32768   // 512K datagrams
 #endif
 inline uint64_t tile_launch_tiles() {
     static long long v = -1;
