@@ -65,6 +65,7 @@ struct BatchParams {
     const uint64_t* tile_prefix;  // packed: exclusive prefix of tile sums (ntiles+1)
     uint64_t* tile_sums;          // packed: scratch, ntiles+1 entries
     uint32_t run_log2;            // wave kernel: datagrams per run = 2^run_log2
+    uint64_t blk0 = 0;            // wave kernel, packed runs of 64: first workgroup of this launch
     int kernel;                   // HYOBFS_KERNEL_* of the context (0 = auto)
 };
 

@@ -277,7 +277,7 @@ salamander_wave_kernel(BatchParams B, KeyParams K) {
     // on neighbouring runs and the chip sweeps memory in address order.
     const uint32_t rl = B.run_log2, RUN = 1u << rl;
     const uint64_t Wt = (uint64_t)gridDim.x * kWavesPerBlock;
-    const uint64_t w = (uint64_t)blockIdx.x * kWavesPerBlock + wid;
+    const uint64_t w = (B.blk0 + blockIdx.x) * kWavesPerBlock + wid;   // (blk0 > 0 only for packed runs of 64)
     const uint32_t j = (uint32_t)lane >> rl, i = (uint32_t)lane & (RUN - 1);
     const uint64_t r = (uint64_t)j * Wt + w;   // this lane's run
     // packed runs of 64: a wave takes DPW consecutive datagrams (lanes 0..DPW-1)
@@ -540,14 +540,37 @@ inline uint32_t wave_run_log2() {
     return (uint32_t)v;
 }
 
+// Workgroups per launch for packed runs of 64 (their waves are independent of the
+// grid size; the slotted runs interleave over the whole grid and stay one launch):
+// HYOBFS_WAVE_LAUNCH_BLOCKS overrides, 0 = one launch (the default: every split measured
+// slower on configs[2], 1.51-1.88 against 1.47 ms, profiles/r03_ab_wave_launch_split.txt;
+// unlike the tile kernel's, these waves live long enough that each launch pays a tail).
+#ifndef HY_WAVE_LAUNCH_BLOCKS
+#define HY_WAVE_LAUNCH_BLOCKS 0
+#endif
+inline uint64_t wave_launch_blocks() {
+    static long long v = -1;
+    if (v < 0) {
+        const char* e = std::getenv("HYOBFS_WAVE_LAUNCH_BLOCKS");
+        v = e ? std::atoll(e) : HY_WAVE_LAUNCH_BLOCKS;
+        if (v < 0) v = 0;
+    }
+    return (uint64_t)v;
+}
+
 template <bool OBF, bool PACKED, int SW>
 void launch_wave_sw(const BatchParams& bp, const KeyParams& k, hipStream_t s) {
     BatchParams b = bp;
     b.run_log2 = PACKED ? wave_packed_run_log2() : wave_run_log2();
-    const uint64_t ngroups = div_up(bp.n, PACKED && b.run_log2 == 6 ? (uint64_t)HY_PACKED_DPW : (uint64_t)kGroup);
+    const bool one_run = PACKED && b.run_log2 == 6;
+    const uint64_t ngroups = div_up(bp.n, one_run ? (uint64_t)HY_PACKED_DPW : (uint64_t)kGroup);
     const uint64_t blocks = div_up(ngroups, kWavesPerBlock);
-    hipLaunchKernelGGL((salamander_wave_kernel<OBF, PACKED, SW>), dim3((uint32_t)blocks),
-                       dim3(kGroup * kWavesPerBlock), 0, s, b, k);
+    const uint64_t per = one_run && wave_launch_blocks() ? wave_launch_blocks() : blocks;
+    for (uint64_t b0 = 0; b0 < blocks; b0 += per) {
+        b.blk0 = b0;
+        hipLaunchKernelGGL((salamander_wave_kernel<OBF, PACKED, SW>), dim3((uint32_t)min(per, blocks - b0)),
+                           dim3(kGroup * kWavesPerBlock), 0, s, b, k);
+    }
 }
 
 }  // namespace hyobfs
