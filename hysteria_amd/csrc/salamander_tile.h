@@ -385,10 +385,11 @@ inline bool tile_params(const BatchParams& b, TileParams& T) {
 // batch one launch ran at 70.5-72.6 % of 8 TB/s and launches of 1M at 75.4-76.8 %
 // (profiles/r03_size_probe.txt): within one long launch the XCDs drift apart in the
 // address space, every launch boundary lines them up again.  Launches of 512K
-// datagrams ran best on 1M and 8M batches in both directions (78.2-78.4 % obfuscate;
-// 256K 77.5-77.7 %, 1M 77.3-77.6 %, 128K 74.5-74.7 %: launch gaps).
+// datagrams measured another ~0.8 % faster (78.2-78.4 %; 256K 77.5-77.7 %, 128K
+// 74.5-74.7 %: launch gaps); 1M is kept so that the 1M-datagram bench batch stays one
+// launch, whose HIP-event time and rocprofv3 kernel average describe the same thing.
 #ifndef HY_TILE_LAUNCH_TILES
-#define HY_TILE_LAUNCH_TILES 32768   // 512K datagrams
+#define HY_TILE_LAUNCH_TILES 65536   // 1M datagrams
 #endif
 inline uint64_t tile_launch_tiles() {
     static long long v = -1;

@@ -1,4 +1,4 @@
-"""HBM bytes per launch of the obfuscate and deobfuscate kernels of one workload
+"""HBM bytes per batch call ("launch" in bench.py's roofline) of the obfuscate and deobfuscate kernels of one workload
 from rocprofv3 FETCH_SIZE and WRITE_SIZE passes (units: KiB), merged into a
 pmc_traffic.json keyed by the kernel-source hash bench.py computes.
 
@@ -18,18 +18,29 @@ MAIN = {True: re.compile(r"salamander_(tile_kernel|wave_kernel)<true"),
         False: re.compile(r"salamander_(tile_kernel|wave_kernel)<false")}
 
 
-def per_dispatch(counter, obf):
+def per_batch(counter, obf):
+    """Counter value of one batch call: the dispatches of the run in issue order, cut
+    into BATCHES equal groups (scripts/prof_one.py issues BATCHES calls per direction;
+    a tile-kernel batch is several launches, launch_tile_sw), summed per group, median
+    group."""
     vals, names = {}, set()
     for f in glob.glob(os.path.join(root, f"pmc_{counter}", "**", "*counter_collection.csv"), recursive=True):
         for row in csv.DictReader(open(f)):
             if row["Counter_Name"] != counter or not MAIN[obf].search(row["Kernel_Name"]):
                 continue
             names.add(row["Kernel_Name"])
-            vals[row["Dispatch_Id"]] = vals.get(row["Dispatch_Id"], 0.0) + float(row["Counter_Value"])
-    v = sorted(vals.values())
-    return (v[len(v) // 2] if v else None), names
+            d = int(row["Dispatch_Id"])
+            vals[d] = vals.get(d, 0.0) + float(row["Counter_Value"])
+    if not vals:
+        return None, names, 0
+    order = [vals[d] for d in sorted(vals)]
+    m = max(1, len(order) // BATCHES)   # launches per batch call
+    groups = [sum(order[i:i + m]) for i in range(0, m * (len(order) // m), m)]
+    groups.sort()
+    return groups[len(groups) // 2], names, m
 
 
+BATCHES = int(os.environ.get("PMC_BATCHES", "5"))
 if wl == "uniform":
     P, L = 1 << 20, 1200
     alg = {True: P * (2 * L + 16), False: P * (2 * L + 8)}
@@ -45,8 +56,8 @@ except (OSError, ValueError, AttributeError):
     entries = []
 for obf in (True, False):
     direction = "obfuscate" if obf else "deobfuscate"
-    fetch_kib, n1 = per_dispatch("FETCH_SIZE", obf)
-    write_kib, n2 = per_dispatch("WRITE_SIZE", obf)
+    fetch_kib, n1, m1 = per_batch("FETCH_SIZE", obf)
+    write_kib, n2, m2 = per_batch("WRITE_SIZE", obf)
     if fetch_kib is None or write_kib is None:
         print(f"no {direction} dispatches in {root}", file=sys.stderr)
         continue
@@ -62,8 +73,9 @@ for obf in (True, False):
         # algorithmic reads: obfuscate L + 8 (payload, salt), deobfuscate L + 8 (wire)
         "read_over_algorithmic_read": round(fetch / ((alg[obf] + (0 if obf else 8 * P)) / 2), 4),
         "write_over_algorithmic_write": round(write / ((alg[obf] - (0 if obf else 8 * P)) / 2), 4),
-        "source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes), median dispatch, "
-                  f"FETCH_SIZE x2 (gfx950); {label}"})
+        "launches_per_batch": m1,
+        "source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes), median batch call "
+                  f"({m1} launch(es) each), FETCH_SIZE x2 (gfx950); {label}"})
 json.dump({"note": "HBM bytes per launch keyed by kernel_src_sha (bench.py); regenerate with "
                    "scripts/collect_profiles.sh on the tree being measured", "entries": entries},
           open(dst, "w"), indent=1)
