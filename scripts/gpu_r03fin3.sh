@@ -5,11 +5,11 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 R=$(pwd)
-O=$R/gpurun_out/r03fin2
+O=$R/gpurun_out/r03fin3
 mkdir -p $O
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest_gpu.log 2>&1 || { echo "pytest failed"; exit 1; }
 timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { echo "smoke failed"; exit 1; }
-bash scripts/collect_profiles.sh r03fin2 > $O/collect.log 2>&1 || { echo "collect failed"; exit 1; }
+bash scripts/collect_profiles.sh r03fin3 > $O/collect.log 2>&1 || { echo "collect failed"; exit 1; }
 cp gpurun_out/profiles/pmc_traffic.json profiles/pmc_traffic.json
 timeout -k 10 300 python -u bench.py > $O/bench.json 2> $O/bench.err || { echo "bench failed"; exit 1; }
 timeout -k 10 300 python -u scripts/aux_bench.py > $O/aux_bench.json 2> $O/aux_bench.err || { echo "aux failed"; exit 1; }
