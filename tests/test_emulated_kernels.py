@@ -45,6 +45,7 @@ SPECS = {
         p["which"], p["args"], {"HYOBFS_PACKED_RUN_LOG2": p["run_log2"], "HYOBFS_RUN_LOG2": p["run_log2"],
                                 "HYOBFS_KERNEL": "wave"}),
     "test_emulated_kernel_vs_oracle": lambda p: (p["which"], p["args"], {"HYEMU_CUS": p["cus"]}),
+    "test_emulated_split_launches": lambda p: (p["which"], p["args"], dict(p["env"])),
 }
 
 
@@ -168,6 +169,25 @@ TILE_CASES = [
 @pytest.mark.parametrize("which,args", TILE_CASES)
 def test_emulated_tile_kernel(emu_lib, which, args):
     _run(emu_lib, which, args, {"HYOBFS_KERNEL": "tile", "HYEMU_CUS": "2"})
+
+
+# A batch split into several launches (salamander_tile.h launch_tile_sw: big batches
+# go out as launches of at most HYOBFS_TILE_LAUNCH_TILES tiles; salamander_wave.h
+# launch_wave_sw: HYOBFS_WAVE_LAUNCH_BLOCKS workgroups for packed batches): tiny limits
+# so every case spans several launches, partial last launches included.
+SPLIT_CASES = [
+    ("uniform", "257 1200 1", (("HYOBFS_KERNEL", "tile"), ("HYOBFS_TILE_LAUNCH_TILES", "3"))),
+    ("uniform", "301 1192 0", (("HYOBFS_KERNEL", "tile"), ("HYOBFS_TILE_LAUNCH_TILES", "5"))),
+    ("slotted", "70 1208 0 8 0 16", (("HYOBFS_KERNEL", "tile"), ("HYOBFS_TILE_LAUNCH_TILES", "1"))),
+    ("bimodal", "3000 1", (("HYOBFS_WAVE_LAUNCH_BLOCKS", "3"),)),
+    ("bimodal", "3000 0", (("HYOBFS_WAVE_LAUNCH_BLOCKS", "2"),)),
+    ("pcap", "4 400 2100 0 100 121", (("HYOBFS_WAVE_LAUNCH_BLOCKS", "1"),)),
+]
+
+
+@pytest.mark.parametrize("which,args,env", SPLIT_CASES)
+def test_emulated_split_launches(emu_lib, which, args, env):
+    _run(emu_lib, which, args, dict(env))
 
 
 @pytest.mark.parametrize("which,args,run_log2", RUN_CASES)
