@@ -20,6 +20,8 @@ HYOBFS_ERR_HIP = -3
 HYOBFS_ERR_NOMEM = -4
 HYOBFS_ERR_NO_DEVICE = -5
 HYOBFS_ERR_IO = -6
+HYOBFS_ERR_CLOSED = -7
+ABI_VERSION = 2   # the HYOBFS_ABI_VERSION these bindings are written for (include/hyobfs.h)
 
 
 class HyobfsBatch(ctypes.Structure):
@@ -107,6 +109,7 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         "hyobfs_salamander_obfuscate_auto": (sz, [pctx, vp, sz, vp, sz]),
         "hyobfs_salamander_deobfuscate": (sz, [pctx, vp, sz, vp, sz]),
         "hyobfs_batch_workspace_size": (u64, [u64]),
+        "hyobfs_salamander_batch_kernel": (i32, [pctx, ctypes.POINTER(HyobfsBatch), i32]),
         "hyobfs_salamander_obfuscate_batch": (i32, [pctx, ctypes.POINTER(HyobfsBatch), vp]),
         "hyobfs_salamander_deobfuscate_batch": (i32, [pctx, ctypes.POINTER(HyobfsBatch), vp]),
         "hyobfs_salamander_obfuscate_batch_sharded": (i32, [vp, ctypes.POINTER(HyobfsBatch), i32]),
@@ -136,6 +139,9 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         f = getattr(lib, name)
         f.restype = res
         f.argtypes = args
+    have = lib.hyobfs_abi_version()
+    if have != ABI_VERSION:   # struct layouts and enum values differ between versions
+        raise OSError(f"{path}: ABI version {have}, these bindings need {ABI_VERSION}: rebuild the library")
     if path == LIB_PATH:
         _lib = lib
     else:

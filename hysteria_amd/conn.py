@@ -72,6 +72,13 @@ def _pyaddr(raw: bytes):
     return raw
 
 
+def _check_conn(status: int, what: str) -> None:
+    """A status call on the connection: HYOBFS_ERR_CLOSED is Go's net.ErrClosed."""
+    if status == _lib.HYOBFS_ERR_CLOSED:
+        raise OSError(errno.EBADF, f"{what}: use of closed connection")
+    check(status, what)
+
+
 def _raise_errno(what: str):
     e = ctypes.get_errno()
     if e in (errno.EAGAIN, errno.EWOULDBLOCK, errno.ETIMEDOUT):
@@ -98,28 +105,42 @@ class SalamanderPacketConn:
         if self._timeout is not None:
             self.settimeout(self._timeout)
         h = ctypes.c_void_p()
+        self._closed = False
         check(self._lib.hyobfs_conn_wrap(sock.fileno(), obfuscator._h, batch, ctypes.byref(h)), "hyobfs_conn_wrap")
         self._h = h
         self.batch = batch
 
     # ------------------------------------------------------------ lifecycle
     def close(self) -> None:
-        if getattr(self, "_h", None):
-            h, self._h = self._h, None
-            self._sock.detach()            # the C side owns and closes the fd
-            check(self._lib.hyobfs_conn_close(h), "hyobfs_conn_close")
+        """Close (conn.go:101-103): the C side sends what a coalescing connection
+        accepted, wakes blocked calls and closes the socket.  Calls made during or
+        after close raise OSError(EBADF) (Go: net.ErrClosed); the handle is freed
+        only when this object goes away (hyobfs_conn_free), so threads still
+        inside a call never touch freed memory.  A second close raises too."""
+        if self._closed:
+            raise OSError(errno.EBADF, "close: use of closed connection")
+        self._closed = True
+        self._sock.detach()            # the C side owns and closes the fd
+        check(self._lib.hyobfs_conn_close(self._h), "hyobfs_conn_close")
 
     def __enter__(self):
         return self
 
     def __exit__(self, *exc):
-        self.close()
+        if not self._closed:
+            self.close()
 
     def __del__(self):
+        h = getattr(self, "_h", None)
+        if not h:
+            return
         try:
-            self.close()
+            if not self._closed:
+                self.close()
         except Exception:
             pass
+        self._h = None
+        self._lib.hyobfs_conn_free(h)   # nobody can be inside a call: this object is unreachable
 
     # ------------------------------------------------------------ net.PacketConn
     def local_addr(self):
@@ -138,13 +159,13 @@ class SalamanderPacketConn:
 
     def set_read_deadline(self, t: float | None) -> None:
         """SetReadDeadline: absolute time (time.time() seconds) or None; applies to blocked reads too."""
-        check(self._lib.hyobfs_conn_set_read_deadline(self._h, 0 if t is None else max(1, int(t * 1e9))),
-              "set_read_deadline")
+        _check_conn(self._lib.hyobfs_conn_set_read_deadline(self._h, 0 if t is None else max(1, int(t * 1e9))),
+                    "set_read_deadline")
 
     def set_write_deadline(self, t: float | None) -> None:
         """SetWriteDeadline: absolute time (time.time() seconds) or None."""
-        check(self._lib.hyobfs_conn_set_write_deadline(self._h, 0 if t is None else max(1, int(t * 1e9))),
-              "set_write_deadline")
+        _check_conn(self._lib.hyobfs_conn_set_write_deadline(self._h, 0 if t is None else max(1, int(t * 1e9))),
+                    "set_write_deadline")
 
     def set_deadline(self, t: float | None) -> None:
         """SetDeadline: both deadlines."""
@@ -182,11 +203,11 @@ class SalamanderPacketConn:
         """Serve the per-datagram write_to / read_from from GPU batches (include/hyobfs_conn.h,
         hyobfs_conn_set_coalescing): write_to returns once the datagram is queued; many
         threads may call both.  The batched calls are unavailable afterwards."""
-        check(self._lib.hyobfs_conn_set_coalescing(self._h, max_batch, max_wait_us), "set_coalescing")
+        _check_conn(self._lib.hyobfs_conn_set_coalescing(self._h, max_batch, max_wait_us), "set_coalescing")
 
     def flush(self) -> None:
         """Wait until every datagram write_to accepted was handed to the socket."""
-        check(self._lib.hyobfs_conn_flush(self._h), "flush")
+        _check_conn(self._lib.hyobfs_conn_flush(self._h), "flush")
 
     def stats(self) -> dict:
         out = (ctypes.c_uint64 * 6)()

@@ -21,8 +21,12 @@
 //     ReadFrom (conn.go:77-86).  The socket's SO_RCVTIMEO bounds the wait (one
 //     absolute deadline per call, like SetReadDeadline).
 //   * shutdown: stop() sends what was accepted, wakes every caller blocked in
-//     ReadFrom / WriteTo (they return -1, EBADF) and joins the threads; the
-//     memory is freed only once no caller is left inside.
+//     ReadFrom / WriteTo (they return -1, EBADF) and joins the threads.  A
+//     writer takes its slot under the spin lock and checks `stop` there: the
+//     flusher's last look for pending datagrams happens under the same lock
+//     after it saw `stop`, so a datagram is either refused (EBADF) or sent --
+//     never accepted and dropped.  The memory is freed only once no caller is
+//     left inside.
 #include "conn_coalesce.h"
 
 #include <errno.h>
@@ -149,7 +153,8 @@ struct Coalescer {
     std::mutex rx_mu;
     std::condition_variable cv_ready, cv_free;
     std::deque<int> ready, freelist;
-    int rx_err = 0;
+    int rx_err = 0;                      // transient receive error, reported once
+    int rx_fatal = 0;                    // the socket is unusable (EBADF, ENOTSOCK, ...): every later read
     std::atomic<uint64_t> received{0}, rx_batches{0}, rx_dropped{0};
     std::thread reader;
     std::atomic<int> callers{0};         // threads inside coalescer_read / coalescer_write
@@ -286,11 +291,15 @@ void Coalescer::read_loop() {
             if (k < 0 && errno != EAGAIN && errno != EWOULDBLOCK && errno != EINTR) {
                 const int e = errno;
                 std::unique_lock<std::mutex> lk(rx_mu);
-                rx_err = e;   // reported by ReadFrom once the queue is empty
-                cv_ready.notify_all();
-                // the socket is gone (closed under us): park until stop instead of
-                // spinning on POLLNVAL; other errors back off briefly
+                // the socket is gone (closed under us): every later ReadFrom fails with
+                // it (Go: net.ErrClosed each time), the thread parks until stop instead
+                // of spinning on POLLNVAL; other errors are reported once, then retried
                 const bool fatal = e == EBADF || e == ENOTSOCK || e == EINVAL || e == EFAULT;
+                if (fatal)
+                    rx_fatal = e;
+                else
+                    rx_err = e;   // reported by ReadFrom once the queue is empty
+                cv_ready.notify_all();
                 cv_free.wait_for(lk, fatal ? std::chrono::hours(24) : std::chrono::milliseconds(1),
                                  [&] { return stop.load(); });
                 break;
@@ -376,7 +385,7 @@ void coalescer_free(Coalescer* q) {
     coalescer_stop(q);
     // callers woken by stop leave through the mutexes and condition variables
     // of q: free it only once the last one is out
-    while (q->callers.load(std::memory_order_acquire) > 0) {
+    while (q->callers.load(std::memory_order_seq_cst) > 0) {
         q->cv_space.notify_all();
         q->cv_ready.notify_all();
         std::this_thread::yield();
@@ -389,8 +398,8 @@ void coalescer_free(Coalescer* q) {
 namespace {
 struct CallerGuard {   // counts a caller inside the coalescer (see coalescer_free)
     Coalescer* q;
-    explicit CallerGuard(Coalescer* c) : q(c) { q->callers.fetch_add(1, std::memory_order_acq_rel); }
-    ~CallerGuard() { q->callers.fetch_sub(1, std::memory_order_acq_rel); }
+    explicit CallerGuard(Coalescer* c) : q(c) { q->callers.fetch_add(1, std::memory_order_seq_cst); }
+    ~CallerGuard() { q->callers.fetch_sub(1, std::memory_order_seq_cst); }
 };
 }  // namespace
 
@@ -400,7 +409,7 @@ int64_t coalescer_write(Coalescer* q, const uint8_t* p, size_t len, const void* 
         errno = EINVAL;
         return -1;
     }
-    if (q->stop) {
+    if (q->stop.load()) {   // early out; the check that counts is the one under the spin lock
         errno = EBADF;
         return -1;
     }
@@ -419,6 +428,11 @@ int64_t coalescer_write(Coalescer* q, const uint8_t* p, size_t len, const void* 
     uint32_t idx;
     for (;;) {
         q->spin.lock();
+        if (q->stop.load()) {   // the flusher may have looked for the last time: refuse
+            q->spin.unlock();
+            errno = EBADF;
+            return -1;
+        }
         b = &q->tx[q->cur];
         if (q->has_space()) {
             idx = b->count++;
@@ -477,6 +491,10 @@ int64_t coalescer_read(Coalescer* q, uint8_t* p, size_t cap, void* addr, uint32_
         {
             std::unique_lock<std::mutex> lk(q->rx_mu);
             while (q->ready.empty()) {
+                if (q->rx_fatal) {
+                    errno = q->rx_fatal;
+                    return -1;
+                }
                 if (q->rx_err) {
                     errno = q->rx_err;
                     q->rx_err = 0;
@@ -486,7 +504,7 @@ int64_t coalescer_read(Coalescer* q, uint8_t* p, size_t cap, void* addr, uint32_
                     errno = EBADF;
                     return -1;
                 }
-                auto woken = [&] { return !q->ready.empty() || q->rx_err || q->stop; };
+                auto woken = [&] { return !q->ready.empty() || q->rx_err || q->rx_fatal || q->stop; };
                 if (q->dl->read.load(std::memory_order_acquire)) {
                     if (!wait_deadline(q->cv_ready, lk, q->dl->read, woken)) {
                         errno = EAGAIN;
@@ -539,6 +557,7 @@ void coalescer_poke(Coalescer* q) {
 }
 
 int coalescer_flush(Coalescer* q) {
+    // every accepted datagram is sent: by the flusher, or by stop() before it exits
     const uint64_t target = q->accepted.load();
     {
         std::lock_guard<std::mutex> lk(q->tx_mu);

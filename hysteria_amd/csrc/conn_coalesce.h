@@ -20,6 +20,12 @@ struct Deadlines {
 };
 int64_t realtime_ns();
 
+// Context lifetime (hyobfs_api.cpp): a connection retains its context, so
+// hyobfs_salamander_free (a Go finalizer, say) never frees it under a live
+// connection; the last release destroys it.
+void ctx_retain(hyobfs_salamander* ctx);
+void ctx_release(hyobfs_salamander* ctx);
+
 // Starts the flusher and reader threads on fd.  nullptr on allocation failure.
 Coalescer* coalescer_new(int fd, hyobfs_salamander* ctx, uint32_t max_batch, uint32_t max_wait_us,
                          const Deadlines* dl);

@@ -61,6 +61,8 @@ struct GeckoGroup {             // one wave's 64 frames, in LDS
 // (constants, 8 key words, 32-bit counter, 3 nonce words), each 64-byte block's
 // bytes in column order: keystream bytes 64 blk + 16 c .. + 15 are state words c,
 // c + 4, c + 8, c + 12.  Pad byte j of frame i is keystream byte out_off[i] + 13 + j.
+// The block index is 64-bit: its low word is the counter, its high word is XORed
+// into nonce word 0, so offsets past 256 GiB never repeat a block.
 // Column order lets four lanes compute one block, a column each, with no transpose.
 #ifndef HY_GK_PAD_ROUNDS
 #define HY_GK_PAD_ROUNDS 8
@@ -94,11 +96,11 @@ __device__ __forceinline__ uint32_t gk_sel4(uint32_t x0, uint32_t x1, uint32_t x
 // Column qi (= this lane's place in its quad) of keystream block blk: the four lanes
 // of a quad compute one block, a column each, the diagonal step by DPP quad
 // permutes.  Every lane of the wave must execute it (the permutes read neighbours).
-__device__ __forceinline__ gk_u128 gk_ks_quad(const GkPad& P, uint32_t blk, uint32_t qi) {
+__device__ __forceinline__ gk_u128 gk_ks_quad(const GkPad& P, uint64_t blk, uint32_t qi) {
     const uint32_t a0 = gk_sel4(kChaC0, kChaC1, kChaC2, kChaC3, qi);
     const uint32_t b0 = gk_sel4(P.k[0], P.k[1], P.k[2], P.k[3], qi);
     const uint32_t c0 = gk_sel4(P.k[4], P.k[5], P.k[6], P.k[7], qi);
-    const uint32_t d0 = gk_sel4(blk, P.n[0], P.n[1], P.n[2], qi);
+    const uint32_t d0 = gk_sel4((uint32_t)blk, P.n[0] ^ (uint32_t)(blk >> 32), P.n[1], P.n[2], qi);
     uint32_t a = a0, b = b0, c = c0, d = d0;
 #pragma unroll
     for (int r = 0; r < HY_GK_PAD_ROUNDS / 2; ++r) {
@@ -115,9 +117,9 @@ __device__ __forceinline__ gk_u128 gk_ks_quad(const GkPad& P, uint32_t blk, uint
 }
 
 // The same column computed by one lane alone (edge chunks, divergent code).
-__device__ __forceinline__ gk_u128 gk_ks_single(const GkPad& P, uint32_t blk, uint32_t col) {
+__device__ __forceinline__ gk_u128 gk_ks_single(const GkPad& P, uint64_t blk, uint32_t col) {
     uint32_t x[16] = {kChaC0, kChaC1, kChaC2, kChaC3, P.k[0], P.k[1], P.k[2], P.k[3],
-                      P.k[4], P.k[5], P.k[6], P.k[7], blk,    P.n[0], P.n[1], P.n[2]};
+                      P.k[4], P.k[5], P.k[6], P.k[7], (uint32_t)blk, P.n[0] ^ (uint32_t)(blk >> 32), P.n[1], P.n[2]};
     uint32_t s[16];
 #pragma unroll
     for (int i = 0; i < 16; ++i) s[i] = x[i];
@@ -143,9 +145,9 @@ __device__ __forceinline__ gk_u128 gk_ks_single(const GkPad& P, uint32_t blk, ui
 __device__ __forceinline__ gk_u128 gk_ks_at(const GkPad& P, uint64_t W0) {
     const uint64_t c0 = W0 & ~15ull;
     const uint32_t sh = (uint32_t)(W0 & 15);
-    const gk_u128 x0 = gk_ks_single(P, (uint32_t)(c0 >> 6), (uint32_t)(c0 >> 4) & 3u);
+    const gk_u128 x0 = gk_ks_single(P, c0 >> 6, (uint32_t)(c0 >> 4) & 3u);
     if (!sh) return x0;
-    const gk_u128 x1 = gk_ks_single(P, (uint32_t)((c0 + 16) >> 6), (uint32_t)((c0 + 16) >> 4) & 3u);
+    const gk_u128 x1 = gk_ks_single(P, (c0 + 16) >> 6, (uint32_t)((c0 + 16) >> 4) & 3u);
     return (x0 >> (8 * sh)) | (x1 << (8 * (16 - sh)));
 }
 
@@ -172,7 +174,7 @@ __device__ __forceinline__ void gk_contrib(const hyobfs_gecko_batch& B, const Gk
         }
         const int32_t plo = max(p0, (int32_t)HYOBFS_GECKO_HEADER_LEN), phi = min(p0 + 16, hp);
         if (plo < phi)   // the 16-aligned wire chunk at base + a is one keystream column
-            X |= gk_ks_single(P, (uint32_t)((base + a) >> 6), (uint32_t)((base + a) >> 4) & 3u) &
+            X |= gk_ks_single(P, (base + a) >> 6, (uint32_t)((base + a) >> 4) & 3u) &
                  gk_mask(plo - p0, phi - p0);
         const int32_t clo = max(p0, hp);
         if (clo < xhi) {   // chunk bytes
@@ -237,11 +239,7 @@ __device__ __forceinline__ void gecko_encode_aligned(const KeyParams& K, const h
     // still in the L2 when the sweep's streaming stores complete it): the first two (salt, header), the one holding
     // the padding/chunk seam, the last; a chunk an earlier frame reaches into is that
     // frame's, and its owner merges every frame that touches it
-#ifdef HY_X_NOEDGE   // ablation builds only (timing experiments; wrong output)
-    if (false) {
-#else
     if (valid) {
-#endif
         const uint32_t hp = G.hp_plain[lane] & 0xffff;
         const uint32_t cs = rs >> 4, ce = (rs + HYOBFS_SALT_LEN + plain - 1) >> 4;
         const uint32_t seam = (rs + HYOBFS_SALT_LEN + hp - 1) >> 4;
@@ -305,11 +303,7 @@ __device__ __forceinline__ void gecko_encode_aligned(const KeyParams& K, const h
             const bool pad = S.kind[u] == 1;
             if (__ballot(pad)) {   // the whole wave: a quad computes one 64-byte block
                 const uint32_t c = T + lane + 64 * u;
-#ifdef HY_X_NOKS   // ablation builds only (timing experiments; wrong output)
-                const gk_u128 ks = (gk_u128)(base + 16ull * c);
-#else
-                const gk_u128 ks = gk_ks_quad(P, (uint32_t)((base + 16ull * c) >> 6), lane & 3u);
-#endif
+                const gk_u128 ks = gk_ks_quad(P, (base + 16ull * c) >> 6, lane & 3u);
                 if (pad) store16_stream(ob + 16 * c, ks ^ G.key[2 * S.kq[u] + (c & 1)]);
             }
         }
@@ -390,11 +384,7 @@ __global__ __launch_bounds__(256) HY_GK_ATTR void gecko_encode_kernel(KeyParams 
             salt = B.salts[f];
             // keyLocked (salamander.go:88-91) in registers; the hash overlaps other waves' sweeps
             uint64_t kw[4];
-#ifdef HY_X_NOGKHASH   // ablation builds only (timing experiments; wrong output)
-            kw[0] = salt; kw[1] = salt * 3; kw[2] = salt ^ 7; kw[3] = salt + 1;
-#else
             wave_key<SW>(K, salt, kw);
-#endif
             k0 = (gk_u128)kw[1] << 64 | kw[0];
             k1 = (gk_u128)kw[3] << 64 | kw[2];
         }
@@ -444,20 +434,12 @@ __global__ __launch_bounds__(256) HY_GK_ATTR void gecko_encode_kernel(KeyParams 
     };
     const GkPad P = gk_pad_params(B);
     auto pad16 = [&](uint32_t k, uint32_t p) -> gk_u128 {   // keystream at plaintext [p, p+16) of frame f0+k
-#ifdef HY_X_NOPAD   // ablation builds only (timing experiments; wrong output)
-        return (gk_u128)(f0 + k + p);
-#else
         return gk_ks_at(P, G.out_off[k] + HYOBFS_SALT_LEN + p);
-#endif
     };
     auto store = [&](uint32_t k, uint32_t p, uint32_t plain, gk_u128 v) {
         uint8_t* __restrict__ po = B.out + G.out_off[k] + HYOBFS_SALT_LEN;
         if (p + 16 <= plain) {
-#ifdef HY_X_ALIGNST   // ablation builds only (timing experiments; wrong output)
-            gk_store16u((uint8_t*)((uintptr_t)(po + p) & ~(uintptr_t)15), v);
-#else
             gk_store16u(po + p, v);
-#endif
         } else {   // the frame's last partial window
             for (uint32_t j = p; j < plain; ++j) po[j] = (uint8_t)(v >> (8 * (j - p)));
         }
@@ -513,7 +495,7 @@ __global__ __launch_bounds__(256) HY_GK_ATTR void gecko_encode_kernel(KeyParams 
     // it steps over the frames started since its previous window (one or two LDS
     // reads for frames of >= 32 windows) instead of a fresh 6-step search.  Edge
     // windows come after the sweep: storing each inside the iteration whose range
-    // holds it (HY_GK_EDGES_INLINE, meant to let lines split between a frame's
+    // holds it (an A/B build, since removed, meant to let lines split between a frame's
     // interior and its edges leave the L2 whole) made the sweep divergent, 0.616 ->
     // 0.826 ms (profiles/r01_ab_gecko/).
     uint32_t q = 0;
@@ -525,16 +507,8 @@ __global__ __launch_bounds__(256) HY_GK_ATTR void gecko_encode_kernel(KeyParams 
 #pragma unroll
         for (int u = 0; u < kGkU; ++u) {   // all windows' loads first
             const uint32_t t = t0 + 64 * u;
-#ifdef HY_GK_BSEARCH   // A/B builds only: the per-window binary search
-            q = 0;
-            if (t < tw) {
-#pragma unroll
-                for (uint32_t step = 32; step; step >>= 1) q = (G.wstart[q + step] <= t) ? q + step : q;
-            }
-#else
             if (t < tw)   // wstart[64] = tw > t stops the walk at frame 63
                 while (G.wstart[q + 1] <= t) ++q;
-#endif
             const uint32_t wi = t - G.wstart[q], p = 16 * wi;
             const uint32_t hpl = G.hp_plain[q], hp = hpl & 0xffff, plain = hpl >> 16;
             kk[u] = q;
@@ -549,20 +523,8 @@ __global__ __launch_bounds__(256) HY_GK_ATTR void gecko_encode_kernel(KeyParams 
 #pragma unroll
         for (int u = 0; u < kGkU; ++u)
             if (ok[u]) store(kk[u], pp[u], 0xFFFFFFFFu, v[u]);
-#ifdef HY_GK_EDGES_INLINE   // A/B builds only: edges stored inside the sweep iteration
-        if (emask) {
-            const uint32_t ws = G.wstart[lane];
-            uint32_t m = 0;
-#pragma unroll
-            for (int c = 0; c < 4; ++c)
-                if ((emask >> c & 1) && ws + cand(c) - T < 64u * kGkU) m |= 1u << c;
-            edges(m);
-        }
-#endif
     }
-#ifndef HY_GK_EDGES_INLINE   // ---- 3. all edge windows after the sweep
-    edges(emask);
-#endif
+    edges(emask);   // ---- 3. all edge windows after the sweep
 }
 
 __global__ __launch_bounds__(256) void gecko_parse_kernel(const uint8_t* in, const uint64_t* in_off,

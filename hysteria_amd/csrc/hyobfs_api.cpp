@@ -12,6 +12,7 @@
 #endif
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -21,12 +22,14 @@
 #include <vector>
 
 #include "../../include/hyobfs.h"
+#include "conn_coalesce.h"
 #include "kernels.h"
 
 using hyobfs::BatchParams;
 using hyobfs::KeyParams;
 
 struct hyobfs_salamander {
+    std::atomic<int> refs{1};   // the caller's reference + one per connection (hyobfs::ctx_retain)
     std::vector<uint8_t> psk;
     int device = 0;
     KeyParams kp{};
@@ -246,8 +249,8 @@ hipMemPool_t scratch_pool(hyobfs_salamander* c) {
     return p;
 }
 
-int validate_and_fill(hyobfs_salamander* c, const hyobfs_batch* b, bool obf, BatchParams& bp,
-                      hipStream_t s) {
+// The launch parameters of a batch (no device call).
+int fill_params(hyobfs_salamander* c, const hyobfs_batch* b, bool obf, BatchParams& bp) {
     if (!c || !b) return HYOBFS_ERR_INVALID;
     if (b->n && (!b->in || !b->out)) return HYOBFS_ERR_INVALID;
     if (obf && b->n && !b->salts) return HYOBFS_ERR_INVALID;
@@ -271,12 +274,19 @@ int validate_and_fill(hyobfs_salamander* c, const hyobfs_batch* b, bool obf, Bat
     bp.out_len = b->out_len;
     bp.out_total = reinterpret_cast<unsigned long long*>(b->out_total);
     bp.kernel = c->kernel;
-    if (b->out_total && hipMemsetAsync(b->out_total, 0, sizeof(uint64_t), s) != hipSuccess)
-        return HYOBFS_ERR_HIP;
     if (b->n && b->out_stride == 0 && b->workspace) {   // packed: caller's tile-sum scratch
         if (b->workspace_bytes < hyobfs_batch_workspace_size(b->n)) return HYOBFS_ERR_INVALID;
         bp.tile_sums = static_cast<uint64_t*>(b->workspace);
     }
+    return HYOBFS_OK;
+}
+
+int validate_and_fill(hyobfs_salamander* c, const hyobfs_batch* b, bool obf, BatchParams& bp,
+                      hipStream_t s) {
+    const int rc = fill_params(c, b, obf, bp);
+    if (rc != HYOBFS_OK) return rc;
+    if (b->out_total && hipMemsetAsync(b->out_total, 0, sizeof(uint64_t), s) != hipSuccess)
+        return HYOBFS_ERR_HIP;
     return HYOBFS_OK;
 }
 
@@ -442,6 +452,7 @@ const char* hyobfs_status_string(int st) {
         case HYOBFS_ERR_NOMEM: return "out of memory";
         case HYOBFS_ERR_NO_DEVICE: return "no usable gfx950 device";
         case HYOBFS_ERR_IO: return "socket I/O error";
+        case HYOBFS_ERR_CLOSED: return "use of closed connection";
         default: return "unknown status";
     }
 }
@@ -474,8 +485,12 @@ int hyobfs_salamander_new(const uint8_t* psk, size_t psk_len, int device, hyobfs
     return HYOBFS_OK;
 }
 
-void hyobfs_salamander_free(hyobfs_salamander* c) {
-    if (!c) return;
+}  // extern "C"
+
+namespace hyobfs {
+void ctx_retain(hyobfs_salamander* c) { c->refs.fetch_add(1, std::memory_order_relaxed); }
+void ctx_release(hyobfs_salamander* c) {
+    if (!c || c->refs.fetch_sub(1, std::memory_order_acq_rel) != 1) return;
     {
         DeviceGuard g(c->device);
         if (c->stream) {
@@ -504,6 +519,13 @@ void hyobfs_salamander_free(hyobfs_salamander* c) {
     }
     delete c;
 }
+}  // namespace hyobfs
+
+extern "C" {
+
+// The caller's reference; a connection still using the context keeps it alive
+// until that connection is freed (hyobfs_conn_free).
+void hyobfs_salamander_free(hyobfs_salamander* c) { hyobfs::ctx_release(c); }
 
 int hyobfs_salamander_device(const hyobfs_salamander* c) { return c ? c->device : -1; }
 
@@ -591,6 +613,12 @@ uint64_t hyobfs_batch_workspace_size(uint64_t n) {
     return (ntiles + 1) * sizeof(uint64_t);
 }
 
+int hyobfs_salamander_batch_kernel(hyobfs_salamander* c, const hyobfs_batch* b, int obfuscate) {
+    BatchParams bp;
+    const int rc = fill_params(c, b, obfuscate != 0, bp);
+    return rc != HYOBFS_OK ? rc : hyobfs::batch_kernel(obfuscate != 0, bp);
+}
+
 int hyobfs_salamander_obfuscate_batch(hyobfs_salamander* c, const hyobfs_batch* b, void* stream) {
     return run_batch(c, b, stream, true);
 }
@@ -629,17 +657,20 @@ int hyobfs_shard_bounds(const uint32_t* in_len, uint64_t n, int nshards, uint64_
     return HYOBFS_OK;
 }
 
-#ifdef HY_GK_KEYS_KERNEL   // A/B builds only: keys from a separate keys pass
-uint64_t hyobfs_gecko_workspace_size(uint64_t n) { return 32 * n; }
-#else   // the shipped kernel derives keys in registers: no workspace
+// the encode kernel derives keys in registers: no workspace
 uint64_t hyobfs_gecko_workspace_size(uint64_t) { return 0; }
-#endif
 
 int hyobfs_gecko_encode_batch(hyobfs_salamander* c, const hyobfs_gecko_batch* b, void* stream) {
     if (!c || !b) return HYOBFS_ERR_INVALID;
     if (b->n == 0) return HYOBFS_OK;
     if (!b->msg || !b->frames || !b->salts || !b->out || !b->out_off)
         return HYOBFS_ERR_INVALID;
+    // an all-zero pad key: a caller that zero-initialised the struct and set no key
+    // would get identical, predictable padding in every batch (the reference's pad
+    // bytes come from crypto/rand, gecko_frame.go:55)
+    bool zero_key = true;
+    for (int i = 0; i < 32; ++i) zero_key = zero_key && b->pad_key[i] == 0;
+    if (zero_key) return HYOBFS_ERR_INVALID;
     const uint64_t ws_need = hyobfs_gecko_workspace_size(b->n);
     if (ws_need && (!b->workspace || b->workspace_bytes < ws_need)) return HYOBFS_ERR_INVALID;
     DeviceGuard g(c->device);

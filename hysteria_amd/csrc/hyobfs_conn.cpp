@@ -52,7 +52,7 @@ struct Ring {   // pinned, device-mapped slots of kBuf bytes
 
 struct hyobfs_conn {
     int fd = -1;
-    hyobfs_salamander* ctx = nullptr;
+    hyobfs_salamander* ctx = nullptr;      // retained (hyobfs::ctx_retain) until the connection is freed
     std::mutex read_mu, write_mu;          // readMutex / writeMutex, conn.go:25-28
     uint8_t read_buf[kBuf];                // readBuf
     uint8_t write_buf[kBuf];               // writeBuf
@@ -62,31 +62,41 @@ struct hyobfs_conn {
     std::vector<sockaddr_storage> raddr;
     hyobfs::Coalescer* co = nullptr;       // set: per-datagram calls go through batches
     hyobfs::Deadlines dl;                  // SetReadDeadline / SetWriteDeadline (absolute, 0 = none)
-    std::atomic<bool> closing{false};      // Close() has begun: calls return -1, EBADF
-    std::atomic<int> inflight{0};          // threads inside read_from / write_to / *_batch
+    std::mutex life_mu;                    // close / free / set_coalescing against each other
+    std::atomic<bool> closing{false};      // Close() (or free) has begun: calls return -1, EBADF
+    std::atomic<int> inflight{0};          // threads inside a call on the connection
 };
 
 namespace {
-struct InFlight {   // a call in progress on the connection (close waits for it to leave)
+// A call in progress on the connection.  Close publishes `closing` and then waits
+// for `inflight` to drain; a caller publishes its increment and then reads
+// `closing`.  Both pairs are sequentially consistent (a store followed by a load
+// of another variable: release/acquire would let either side miss the other,
+// x86's store buffer does exactly that), so a caller either sees `closing` and
+// leaves without touching the connection's state, or the closer sees the caller
+// and waits for it.  The memory itself is freed only by hyobfs_conn_free, which
+// no call may race (include/hyobfs_conn.h).
+struct InFlight {
     hyobfs_conn* c;
-    explicit InFlight(hyobfs_conn* x) : c(x) { c->inflight.fetch_add(1, std::memory_order_acq_rel); }
-    ~InFlight() { c->inflight.fetch_sub(1, std::memory_order_acq_rel); }
+    explicit InFlight(hyobfs_conn* x) : c(x) { c->inflight.fetch_add(1, std::memory_order_seq_cst); }
+    ~InFlight() { c->inflight.fetch_sub(1, std::memory_order_seq_cst); }
     bool closed() const {
-        if (!c->closing.load(std::memory_order_acquire)) return false;
+        if (!c->closing.load(std::memory_order_seq_cst)) return false;
         errno = EBADF;
         return true;
     }
 };
 
 // Stops the coalescer (it sends what WriteTo accepted while the socket is still
-// open), then waits for every caller still inside the connection.
+// open), then waits for every caller still inside the connection.  Caller holds
+// life_mu and has checked that the connection is not closing yet.
 void quiesce(hyobfs_conn* c, bool wake_readers) {
-    c->closing.store(true, std::memory_order_release);
+    c->closing.store(true, std::memory_order_seq_cst);
     hyobfs::coalescer_stop(c->co);
-    // a plain-mode ReadFrom blocked in recvfrom: shutdown wakes it (a 0-byte
-    // read, turned into EBADF below); Linux does this for unconnected UDP too
+    // a plain-mode ReadFrom blocked in poll: shutdown wakes it (a 0-byte read,
+    // turned into EBADF below); Linux does this for unconnected UDP too
     if (wake_readers) (void)shutdown(c->fd, SHUT_RD);
-    while (c->inflight.load(std::memory_order_acquire) > 0) std::this_thread::yield();
+    while (c->inflight.load(std::memory_order_seq_cst) > 0) std::this_thread::yield();
 }
 }  // namespace
 
@@ -110,31 +120,39 @@ int hyobfs_conn_wrap(int fd, hyobfs_salamander* ctx, uint32_t batch, hyobfs_conn
     c->riov.resize(batch);
     c->wiov.resize(batch);
     c->raddr.resize(batch);
+    hyobfs::ctx_retain(ctx);   // the context outlives every connection on it (hyobfs_salamander_free)
     *out = c;
     return HYOBFS_OK;
 }
 
-static void conn_release(hyobfs_conn* c) {
-    hyobfs::coalescer_free(c->co);   // (already stopped by quiesce)
-    c->rx.release();
-    c->tx.release();
-    delete c;
+// Close(), conn.go:101-103, which closes the inner conn: later calls fail with
+// EBADF (Go: net.ErrClosed).  The coalescer first sends every datagram WriteTo
+// accepted, then its threads stop; threads blocked in calls are woken; the fd
+// closes once no thread of ours can touch it.  The memory stays until
+// hyobfs_conn_free, so calls racing or following Close never see freed state.
+int hyobfs_conn_close(hyobfs_conn* c) {
+    if (!c) return HYOBFS_ERR_INVALID;
+    std::lock_guard<std::mutex> lk(c->life_mu);
+    if (c->closing.load(std::memory_order_seq_cst)) {
+        errno = EBADF;
+        return HYOBFS_ERR_CLOSED;   // Go: a second Close returns an error too
+    }
+    quiesce(c, true);
+    const int rc = close(c->fd);
+    return rc == 0 ? HYOBFS_OK : HYOBFS_ERR_IO;
 }
 
 void hyobfs_conn_free(hyobfs_conn* c) {
     if (!c) return;
-    quiesce(c, false);   // sends what WriteTo accepted, stops the coalescer's threads
-    conn_release(c);
-}
-
-int hyobfs_conn_close(hyobfs_conn* c) {   // Close(), conn.go:101-103: closes the inner conn
-    if (!c) return HYOBFS_ERR_INVALID;
-    // the coalescer flushes before the socket closes: every datagram WriteTo
-    // accepted is sent, and no thread of ours touches the fd number after close
-    quiesce(c, true);
-    const int rc = close(c->fd);
-    conn_release(c);
-    return rc == 0 ? HYOBFS_OK : HYOBFS_ERR_IO;
+    {
+        std::lock_guard<std::mutex> lk(c->life_mu);
+        if (!c->closing.load(std::memory_order_seq_cst)) quiesce(c, false);   // detach: the socket stays open
+    }
+    hyobfs::coalescer_free(c->co);   // (already stopped)
+    c->rx.release();
+    c->tx.release();
+    hyobfs::ctx_release(c->ctx);
+    delete c;
 }
 
 // ReadFrom, conn.go:73-88
@@ -322,13 +340,18 @@ int hyobfs_conn_write_batch(hyobfs_conn* c, const hyobfs_dgram* msgs, uint32_t n
 }
 
 int hyobfs_conn_set_coalescing(hyobfs_conn* c, uint32_t max_batch, uint32_t max_wait_us) {
-    if (!c || c->co || max_batch == 0 || max_batch > (1u << 16)) return HYOBFS_ERR_INVALID;
+    if (!c) return HYOBFS_ERR_INVALID;
+    std::lock_guard<std::mutex> lk(c->life_mu);
+    if (c->closing.load(std::memory_order_seq_cst)) return HYOBFS_ERR_CLOSED;
+    if (c->co || max_batch == 0 || max_batch > (1u << 16)) return HYOBFS_ERR_INVALID;
     c->co = hyobfs::coalescer_new(c->fd, c->ctx, max_batch, max_wait_us, &c->dl);
     return c->co ? HYOBFS_OK : HYOBFS_ERR_NOMEM;
 }
 
 int hyobfs_conn_set_read_deadline(hyobfs_conn* c, int64_t unix_ns) {
     if (!c || unix_ns < 0) return HYOBFS_ERR_INVALID;
+    InFlight g(c);
+    if (g.closed()) return HYOBFS_ERR_CLOSED;
     c->dl.read.store(unix_ns, std::memory_order_release);
     hyobfs::coalescer_poke(c->co);   // blocked reads re-read it (net.Conn: also currently-blocked calls)
     return HYOBFS_OK;
@@ -336,6 +359,8 @@ int hyobfs_conn_set_read_deadline(hyobfs_conn* c, int64_t unix_ns) {
 
 int hyobfs_conn_set_write_deadline(hyobfs_conn* c, int64_t unix_ns) {
     if (!c || unix_ns < 0) return HYOBFS_ERR_INVALID;
+    InFlight g(c);
+    if (g.closed()) return HYOBFS_ERR_CLOSED;
     c->dl.write.store(unix_ns, std::memory_order_release);
     hyobfs::coalescer_poke(c->co);
     return HYOBFS_OK;
@@ -343,10 +368,12 @@ int hyobfs_conn_set_write_deadline(hyobfs_conn* c, int64_t unix_ns) {
 
 int hyobfs_conn_flush(hyobfs_conn* c) {
     if (!c) return HYOBFS_ERR_INVALID;
+    InFlight g(c);
+    if (g.closed()) return HYOBFS_ERR_CLOSED;   // (Close already sent everything accepted)
     return c->co ? hyobfs::coalescer_flush(c->co) : HYOBFS_OK;
 }
 
-int hyobfs_conn_stats(hyobfs_conn* c, uint64_t out[6]) {
+int hyobfs_conn_stats(hyobfs_conn* c, uint64_t out[6]) {   // also after Close: the counters stay
     if (!c || !out) return HYOBFS_ERR_INVALID;
     if (!c->co) {
         for (int i = 0; i < 6; ++i) out[i] = 0;

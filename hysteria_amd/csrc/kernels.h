@@ -73,6 +73,8 @@ struct BatchParams {
 // HYOBFS_KERNEL environment variable, else 0)
 int resolve_kernel(int ctx_kernel);
 hipError_t launch_salamander(bool obfuscate, const BatchParams& b, const KeyParams& k, hipStream_t s);
+// the kernel launch_salamander would run (kKernelTile / kKernelWave; kKernelAuto for an empty batch)
+int batch_kernel(bool obfuscate, const BatchParams& b);
 hipError_t launch_keys(const KeyParams& k, const uint64_t* salts, uint8_t* keys, uint64_t n,
                        hipStream_t s);
 hipError_t launch_gecko_encode(const KeyParams& k, const hyobfs_gecko_batch& b, hipStream_t s);

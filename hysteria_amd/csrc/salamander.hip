@@ -149,13 +149,12 @@ __global__ void synth_bimodal_kernel(uint32_t* dst, uint64_t n, uint64_t seed, u
 // applies (tile_params) and the wave kernel elsewhere; WAVE forces the wave
 // kernel; TILE asks for the tile kernel (falls back to the wave kernel where it
 // does not apply).  HYOBFS_KERNEL=wave|tile sets what AUTO means in a process.
-static int kernel_override() {   // HYOBFS_KERNEL, as HYOBFS_KERNEL_* (0 = auto)
-    static int v = -1;
-    if (v == -1) {
+static int kernel_override() {   // HYOBFS_KERNEL, as HYOBFS_KERNEL_* (0 = auto); read once, thread-safe
+    static const int v = [] {
         const char* e = std::getenv("HYOBFS_KERNEL");
-        v = !e ? kKernelAuto : std::strcmp(e, "wave") == 0 ? kKernelWave : std::strcmp(e, "tile") == 0 ? kKernelTile
-                                                                                                     : kKernelAuto;
-    }
+        return !e ? kKernelAuto : std::strcmp(e, "wave") == 0 ? kKernelWave : std::strcmp(e, "tile") == 0 ? kKernelTile
+                                                                                                        : kKernelAuto;
+    }();
     return v;
 }
 
@@ -184,6 +183,15 @@ static void launch_main(const BatchParams& bp, const KeyParams& k, hipStream_t s
         HY_CASE(15)
 #undef HY_CASE
     }
+}
+
+// Which kernel launch_salamander runs for this batch (HYOBFS_KERNEL_*; no launch).
+int batch_kernel(bool obf, const BatchParams& b) {
+    if (b.n == 0) return kKernelAuto;   // nothing runs
+    TileParams T;
+    const bool tile = b.out_stride != 0 && resolve_kernel(b.kernel) != kKernelWave &&
+                      (obf ? tile_params<true>(b, T) : tile_params<false>(b, T));
+    return tile ? kKernelTile : kKernelWave;
 }
 
 hipError_t launch_salamander(bool obf, const BatchParams& b, const KeyParams& k, hipStream_t s) {

@@ -271,11 +271,7 @@ __global__ __launch_bounds__(256, HY_TILE_MIN_WAVES) void salamander_tile_kernel
         const uint32_t qk = lane >> 2, qi = lane & 3;
         uint64_t salt = 0;
         if (qk < nt) salt = OBF ? B.salts[p0 + qk] : load8_nt(ib + qk * in_stride);
-#if defined(HY_X_NOHASH) || defined(HY_X_TILE_NOHASH)   // ablation builds only (wrong output)
-        const uint64_t kw = salt * (qi + 3);
-#else
         const uint64_t kw = quad_key<SW>(K, salt, qi);
-#endif
         if (qk < nt) {
             s_key[qk * 8 + qi] = kw;
             s_key[qk * 8 + 4 + qi] = kw;
@@ -391,14 +387,13 @@ inline bool tile_params(const BatchParams& b, TileParams& T) {
 #ifndef HY_TILE_LAUNCH_TILES
 #define HY_TILE_LAUNCH_TILES 65536   // 1M datagrams
 #endif
-inline uint64_t tile_launch_tiles() {
-    static long long v = -1;
-    if (v < 0) {
+inline uint64_t tile_launch_tiles() {   // read once, thread-safe (a function-local static)
+    static const uint64_t v = [] {
         const char* e = std::getenv("HYOBFS_TILE_LAUNCH_TILES");
-        v = e ? std::atoll(e) : HY_TILE_LAUNCH_TILES;
-        if (v < 0) v = 0;
-    }
-    return (uint64_t)v;
+        const long long x = e ? std::atoll(e) : HY_TILE_LAUNCH_TILES;
+        return (uint64_t)(x < 0 ? 0 : x);
+    }();
+    return v;
 }
 
 template <bool OBF, int SW>

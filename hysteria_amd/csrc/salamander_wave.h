@@ -370,11 +370,7 @@ salamander_wave_kernel(BatchParams B, KeyParams K) {
     // ---- 2. key, rotated to the output phase
     {
         uint64_t key[4], kr[4];
-#ifdef HY_X_NOHASH   // ablation builds only (timing experiments; wrong output)
-        key[0] = salt; key[1] = salt * 3; key[2] = salt ^ 7; key[3] = salt + 1;
-#else
         wave_key<SW>(K, salt, key);
-#endif
         rotl_key_bytes(key, (rel + SALT) & 31u, kr);
         G.key[2 * lane] = make_uint4((uint32_t)kr[0], (uint32_t)(kr[0] >> 32), (uint32_t)kr[1],
                                      (uint32_t)(kr[1] >> 32));
@@ -394,7 +390,6 @@ salamander_wave_kernel(BatchParams B, KeyParams K) {
         u128 bv[3] = {0, 0, 0};
         const uint32_t pe0 = __shfl_up(incm, 1, 64);   // max region end over earlier datagrams
         const uint32_t pe = lane ? pe0 : 0u;
-#ifndef HY_X_NOBOUND
         if (W) {
             const uint32_t st = rel, en = rel + W;
             const uint32_t cs = st >> 4, ce = (en - 1) >> 4;
@@ -421,9 +416,6 @@ salamander_wave_kernel(BatchParams B, KeyParams K) {
                 }
             }
         }
-#else
-        (void)pe;
-#endif
         const uint32_t np = (uint32_t)__builtin_popcount(parkm);
         const uint32_t base = (uint32_t)wave_incl_scan(np, lane) - np;
         if (base + np > (uint32_t)GroupBuf::kSlots) parkm = 0;   // out of slots: store late
@@ -521,23 +513,19 @@ salamander_wave_kernel(BatchParams B, KeyParams K) {
 #ifndef HY_PACKED_RUN_LOG2
 #define HY_PACKED_RUN_LOG2 6
 #endif
+// Environment knobs are read once per process, thread-safely (function-local statics).
+inline uint32_t env_run_log2(const char* name, int dflt) {
+    const char* e = std::getenv(name);
+    const int v = e ? std::atoi(e) : dflt;
+    return (uint32_t)(v < 0 ? 0 : v > 6 ? 6 : v);
+}
 inline uint32_t wave_packed_run_log2() {   // packed layout: datagrams per run (HYOBFS_PACKED_RUN_LOG2)
-    static int v = -1;
-    if (v < 0) {
-        const char* e = std::getenv("HYOBFS_PACKED_RUN_LOG2");
-        v = e ? std::atoi(e) : HY_PACKED_RUN_LOG2;
-        v = v < 0 ? 0 : v > 6 ? 6 : v;
-    }
-    return (uint32_t)v;
+    static const uint32_t v = env_run_log2("HYOBFS_PACKED_RUN_LOG2", HY_PACKED_RUN_LOG2);
+    return v;
 }
 inline uint32_t wave_run_log2() {
-    static int v = -1;
-    if (v < 0) {
-        const char* e = std::getenv("HYOBFS_RUN_LOG2");
-        v = e ? std::atoi(e) : HY_RUN_LOG2;
-        v = v < 0 ? 0 : v > 6 ? 6 : v;
-    }
-    return (uint32_t)v;
+    static const uint32_t v = env_run_log2("HYOBFS_RUN_LOG2", HY_RUN_LOG2);
+    return v;
 }
 
 // Workgroups per launch for packed runs of 64 (their waves are independent of the
@@ -549,13 +537,12 @@ inline uint32_t wave_run_log2() {
 #define HY_WAVE_LAUNCH_BLOCKS 0
 #endif
 inline uint64_t wave_launch_blocks() {
-    static long long v = -1;
-    if (v < 0) {
+    static const uint64_t v = [] {
         const char* e = std::getenv("HYOBFS_WAVE_LAUNCH_BLOCKS");
-        v = e ? std::atoll(e) : HY_WAVE_LAUNCH_BLOCKS;
-        if (v < 0) v = 0;
-    }
-    return (uint64_t)v;
+        const long long x = e ? std::atoll(e) : HY_WAVE_LAUNCH_BLOCKS;
+        return (uint64_t)(x < 0 ? 0 : x);
+    }();
+    return v;
 }
 
 template <bool OBF, bool PACKED, int SW>

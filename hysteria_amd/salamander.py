@@ -192,6 +192,14 @@ class SalamanderObfuscator:
         f = self._lib.hyobfs_salamander_obfuscate_batch if obf else self._lib.hyobfs_salamander_deobfuscate_batch
         check(f(self._h, ctypes.byref(b), s), "obfuscate_batch" if obf else "deobfuscate_batch")
 
+    def batch_kernel(self, obf: bool, *, inp, n, out, **kw) -> str:
+        """The kernel a batch call with these arguments would run ("tile" / "wave"; "none"
+        for an empty batch): hyobfs_salamander_batch_kernel, no device work."""
+        b = _make_batch(inp=inp, n=n, out=out, **kw)
+        k = self._lib.hyobfs_salamander_batch_kernel(self._h, ctypes.byref(b), int(bool(obf)))
+        check(min(k, 0), "batch_kernel")
+        return {0: "none", 1: "wave", 2: "tile"}[k]
+
     def obfuscate_batch(self, inp, n, *, salts, out, **kw) -> None:
         """Obfuscate n datagrams on the device (layout rules: include/hyobfs.h).
 

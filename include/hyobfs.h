@@ -56,7 +56,16 @@
 extern "C" {
 #endif
 
-#define HYOBFS_ABI_VERSION 1
+/* ABI version.  2 (this header) against 1:
+ *   - struct hyobfs_gecko_batch: pad_seed (u64) became pad_key[32], pad_nonce[12]
+ *     and reserved_ (hyobfs_gecko.h), so the fields after it moved;
+ *   - HYOBFS_KERNEL_* values: 2 is TILE (was PERSISTENT), 3..6 are rejected;
+ *   - hyobfs_conn_close no longer frees the connection: hyobfs_conn_free does
+ *     (include/hyobfs_conn.h), and calls after close fail with EBADF;
+ *   - new status HYOBFS_ERR_CLOSED; a zero Gecko pad key is rejected.
+ * Bindings compare hyobfs_abi_version() with the version they were written
+ * for and refuse a mismatch (hysteria_amd/_lib.py does). */
+#define HYOBFS_ABI_VERSION 2
 
 #define HYOBFS_PSK_MIN_LEN 4  /* smPSKMinLen, salamander.go:14 */
 #define HYOBFS_SALT_LEN 8     /* smSaltLen,   salamander.go:15 */
@@ -71,6 +80,7 @@ extern "C" {
 #define HYOBFS_ERR_NOMEM (-4)         /* allocation failed */
 #define HYOBFS_ERR_NO_DEVICE (-5)     /* no usable gfx950 device */
 #define HYOBFS_ERR_IO (-6)            /* socket error (hyobfs_conn_*); errno kept */
+#define HYOBFS_ERR_CLOSED (-7)        /* call on a closed connection (Go: net.ErrClosed) */
 
 typedef struct hyobfs_salamander hyobfs_salamander; /* opaque context */
 
@@ -90,6 +100,9 @@ int hyobfs_device_count(void);
    `device`.  *out is set only on HYOBFS_OK. */
 int hyobfs_salamander_new(const uint8_t* psk, size_t psk_len, int device,
                           hyobfs_salamander** out);
+/* Drops the caller's reference.  A connection made on the context
+   (hyobfs_conn_wrap) holds its own reference until hyobfs_conn_free, so the
+   context is destroyed only when the last of them goes (any order). */
 void hyobfs_salamander_free(hyobfs_salamander* ctx);
 int hyobfs_salamander_device(const hyobfs_salamander* ctx);
 
@@ -187,6 +200,11 @@ typedef struct hyobfs_batch {
 } hyobfs_batch;
 
 uint64_t hyobfs_batch_workspace_size(uint64_t n);
+/* Which batch kernel a call with this batch would run under the context's
+   setting (HYOBFS_KERNEL_TILE or HYOBFS_KERNEL_WAVE; HYOBFS_KERNEL_AUTO for an
+   empty batch), or a negative status for an invalid batch.  No device work:
+   tests use it to prove which kernel their case exercised. */
+int hyobfs_salamander_batch_kernel(hyobfs_salamander* ctx, const hyobfs_batch* b, int obfuscate);
 int hyobfs_salamander_obfuscate_batch(hyobfs_salamander* ctx, const hyobfs_batch* b,
                                       void* stream);
 int hyobfs_salamander_deobfuscate_batch(hyobfs_salamander* ctx, const hyobfs_batch* b,

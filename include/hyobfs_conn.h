@@ -51,18 +51,23 @@ typedef struct hyobfs_dgram {
     uint32_t pad_;
 } hyobfs_dgram;
 
-/* Wrap a bound UDP socket.  The connection does not own ctx.  batch = the
-   largest number of datagrams per batched call (0 = 1024). */
+/* Wrap a bound UDP socket.  The connection takes a reference on ctx (released
+   by hyobfs_conn_free).  batch = the largest number of datagrams per batched
+   call (0 = 1024). */
 int hyobfs_conn_wrap(int fd, hyobfs_salamander* ctx, uint32_t batch, hyobfs_conn** out);
-/* Close(): sends what a coalescing connection accepted, wakes every thread
-   blocked in a call on the connection (they return -1 with errno EBADF, as a
-   Go ReadFrom returns once Close closes the inner conn), waits for them to
-   leave, closes the socket and frees the connection.  Calls that START after
-   close began are invalid (the handle is gone). */
+/* Close() (conn.go:101-103): shuts the connection down but does NOT free it.
+   A coalescing connection first sends every datagram write_to accepted; every
+   thread blocked in a call on the connection is woken (-1, errno EBADF, as a Go
+   ReadFrom returns net.ErrClosed once Close closes the inner conn); close waits
+   for them to leave, then closes the socket.  Afterwards every call returns
+   -1 / errno EBADF (status calls HYOBFS_ERR_CLOSED), whether it started before
+   or after close -- the handle stays valid until hyobfs_conn_free.  A second
+   close returns HYOBFS_ERR_CLOSED. */
 int hyobfs_conn_close(hyobfs_conn* c);
-/* Frees the connection, leaves the socket open.  Coalescing callers are woken
-   as by close; in plain mode no call may be in progress (nothing wakes a
-   recvfrom on a socket that stays open). */
+/* Frees the connection and releases its context reference.  No call on c may
+   be in progress or start later (a Go finalizer has exactly that guarantee).
+   On a connection that was not closed it detaches first: the coalescer sends
+   what was accepted, its threads stop, and the socket stays open. */
 void hyobfs_conn_free(hyobfs_conn* c);
 
 /* ReadFrom: bytes written to p (>= 0), or -1 with errno set (socket error). */
@@ -111,12 +116,16 @@ int hyobfs_conn_set_write_deadline(hyobfs_conn* c, int64_t unix_ns);
      - many threads may call write_to / read_from at once; the batched calls
        return -1 with errno EBUSY.
    Latency added per datagram: up to max_wait_us plus one GPU batch.  Call once,
-   before the connection is used; hyobfs_conn_free / _close send what was
-   accepted (before _close closes the socket), then stop the threads. */
+   before the connection is used; hyobfs_conn_close / _free send what was
+   accepted (before _close closes the socket), then stop the threads.  A
+   write_to that races close is either refused (EBADF) or sent, never
+   accepted and dropped. */
 int hyobfs_conn_set_coalescing(hyobfs_conn* c, uint32_t max_batch, uint32_t max_wait_us);
-/* Blocks until every datagram write_to accepted so far was handed to the socket. */
+/* Blocks until every datagram write_to accepted so far was handed to the socket
+   (HYOBFS_ERR_CLOSED after close, which has sent them all). */
 int hyobfs_conn_flush(hyobfs_conn* c);
-/* Coalescing counters: accepted, tx batches, tx errors, received, rx batches, rx dropped. */
+/* Coalescing counters: accepted, tx batches, tx errors, received, rx batches, rx
+   dropped (still readable after close). */
 int hyobfs_conn_stats(hyobfs_conn* c, uint64_t out[6]);
 
 #ifdef __cplusplus

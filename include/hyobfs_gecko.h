@@ -101,9 +101,12 @@ typedef struct hyobfs_gecko_batch {
        64-byte block's bytes in column order (bytes 16c..16c+15 = state words c,
        c+4, c+8, c+12 after the final addition).  Pad byte j of frame i is
        keystream byte out_off[i] + 13 + j: its offset in `out`, so every pad byte
-       of a batch takes a different keystream byte (out must stay below 256 GiB).
-       Draw a fresh key per batch (hyobfs_gecko_random_pad_key, getrandom); an
-       explicit key makes the output reproducible (tests, oracle/gecko_ref.py). */
+       of a batch takes a different keystream byte.  Block b (64-bit) uses
+       counter = b mod 2^32 and nonce word 0 XOR (b >> 32): no block repeats at
+       any offset.  Draw a fresh key per batch (hyobfs_gecko_random_pad_key,
+       getrandom); an explicit key makes the output reproducible (tests,
+       oracle/gecko_ref.py).  An all-zero pad_key is rejected
+       (HYOBFS_ERR_INVALID): it is what a caller that forgot the key passes. */
     uint8_t pad_key[32];
     uint8_t pad_nonce[12];
     uint32_t reserved_;
@@ -127,8 +130,8 @@ int hyobfs_gecko_random_pad_key(uint8_t key[32], uint8_t nonce[12]);
  * Asynchronous on `stream` (NULL = null stream).  A frame the reference could
  * not have produced (total chunks outside [2, 8], chunk index >= total, or a
  * datagram longer than HYOBFS_GECKO_BUFFER_SIZE) is skipped on the device: its
- * output bytes are left untouched.  HYOBFS_ERR_INVALID for a missing pointer
- * or a workspace shorter than hyobfs_gecko_workspace_size(n).
+ * output bytes are left untouched.  HYOBFS_ERR_INVALID for a missing pointer,
+ * an all-zero pad_key or a workspace shorter than hyobfs_gecko_workspace_size(n).
  */
 int hyobfs_gecko_encode_batch(hyobfs_salamander* ctx, const hyobfs_gecko_batch* b, void* stream);
 

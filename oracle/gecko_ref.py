@@ -105,8 +105,12 @@ def _rotl(x, n):
 
 
 def chacha_block(key: bytes, counter: int, nonce: bytes, rounds: int = PAD_ROUNDS) -> list[int]:
-    """RFC 8439 2.3 block function with ``rounds`` rounds: the 16 output words."""
-    s = list(CHACHA_C) + list(struct.unpack("<8I", key)) + [counter & 0xFFFFFFFF] + list(struct.unpack("<3I", nonce))
+    """RFC 8439 2.3 block function with ``rounds`` rounds: the 16 output words.  A
+    block index past 32 bits folds its high word into nonce word 0
+    (include/hyobfs_gecko.h), so the keystream never repeats a block."""
+    n0, n1, n2 = struct.unpack("<3I", nonce)
+    s = list(CHACHA_C) + list(struct.unpack("<8I", key)) + [counter & 0xFFFFFFFF,
+                                                            n0 ^ ((counter >> 32) & 0xFFFFFFFF), n1, n2]
     x = list(s)
 
     def qr(a, b, c, d):

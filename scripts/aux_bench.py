@@ -51,7 +51,7 @@ out = torch.empty(total + 16, dtype=torch.uint8, device=dev)
 ws = torch.empty(gecko.workspace_size(nf), dtype=torch.uint8, device=dev)
 o = hysteria_amd.SalamanderObfuscator(b"average_password", 0)
 dfr, doff = d(fr), d(off)
-ms = timed(lambda: gecko.encode_batch(o, msg=msg, frames=dfr, salts=salts, pad_key=bytes(32), pad_nonce=bytes(12), out=out, out_off=doff,
+ms = timed(lambda: gecko.encode_batch(o, msg=msg, frames=dfr, salts=salts, pad_key=bytes(range(1, 33)), pad_nonce=bytes(12), out=out, out_off=doff,
                                       workspace=ws, n=nf))
 alg = M * L + total   # chunk bytes read + wire bytes written (pad generated on device)
 res["gecko_encode"] = {"messages": M, "msg_len": L, "frames": nf, "wire_bytes": total, "ms": round(ms, 4),

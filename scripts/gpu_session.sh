@@ -1,25 +1,56 @@
 #!/bin/bash
-# One GPU-box session: calibration, parity tests, bench, kernel-trace profile.
-# Every GPU step has its own time limit; the first failure ends the script.
+# One GPU-box session, parameterised (replaces the per-session scripts of rounds 1-3):
+#
+#   bash scripts/gpu_session.sh TAG STEP [STEP ...]
+#
+# Results go to gpurun_out/TAG/.  Every GPU step has its own time limit and the
+# first failure ends the script (no retries).  Steps:
+#   test            the whole GPU suite (pytest -m gpu)
+#   test:EXPR       GPU tests matching -k EXPR
+#   smoke           __graft_entry__.smoke()
+#   bench           bench.py (the driver's default line)
+#   trace           rocprofv3 --kernel-trace of the bench command (per-dispatch CSV + stats)
+#   collect         PMC traffic + kernel-trace stats (scripts/collect_profiles.sh TAG)
+#   aux             (f)-row rates (scripts/aux_bench.py)
+#   auxpmc          VALU counters of the (f)-row kernels
+#   host            host-to-host rates (scripts/host_bench.py)
+#   ab              in-process A/B of library builds (scripts/ab_variants.py; AB_* env vars)
+#   abg             the same for Gecko builds (scripts/ab_gecko_variants.py)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 R=$(pwd)
-OUT=$R/gpurun_out
-mkdir -p "$OUT"
-step() { local name=$1 lim=$2; shift 2; echo "== $name"; timeout -k 10 "$lim" "$@"; local rc=$?; echo "== $name rc=$rc"; if [ $rc -ne 0 ]; then exit $rc; fi; }
-MODE=${1:-all}
-if [[ $MODE == *calib* || $MODE == all ]]; then
-  step calib 180 ./tools/hbm_copy > "$OUT/hbm_copy.json"
-fi
-if [[ $MODE == *test* || $MODE == all ]]; then
-  step pytest 700 python -u -m pytest tests -x -v -m gpu --timeout 120 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1
-fi
-if [[ $MODE == *bench* || $MODE == all ]]; then
-  step bench 300 python bench.py --steps 20 --warmup 5 --cpu-seconds 6 > "$OUT/bench.json" 2> "$OUT/bench.err"
-  step bench_bimodal 300 python bench.py --workload bimodal --steps 10 --warmup 3 --no-cpu-baseline --no-parity > "$OUT/bench_bimodal.json" 2> "$OUT/bench_bimodal.err"
-fi
-if [[ $MODE == *prof* || $MODE == all ]]; then
-  cd /tmp && export TMPDIR=/tmp
-  step rocprof 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 "$R/bench.py" --steps 20 --warmup 5 --no-cpu-baseline --no-parity > "$OUT/prof_bench.log" 2>&1
-fi
+TAG=${1:?tag}
+shift
+O=$R/gpurun_out/$TAG
+mkdir -p "$O"
+step() {
+  local name=$1 lim=$2; shift 2
+  echo "== $name $(date +%T)"
+  timeout -k 10 "$lim" "$@"
+  local rc=$?
+  echo "== $name rc=$rc"
+  [ $rc -eq 0 ] || exit $rc
+}
+for s in "$@"; do
+  case $s in
+    test) step test 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
+            > "$O/pytest_gpu.log" 2>&1 ;;
+    test:*) step test 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
+            -k "${s#test:}" > "$O/pytest_gpu_k.log" 2>&1 ;;
+    smoke) step smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()" > "$O/smoke.log" 2>&1 ;;
+    bench) step bench 300 python -u bench.py > "$O/bench.json" 2> "$O/bench.err" ;;
+    trace) (cd /tmp && export TMPDIR=/tmp && step trace 300 rocprofv3 --kernel-trace --stats --output-format csv \
+            -d "$O/trace" -o run -- python3 "$R/bench.py" --steps 20 --warmup 5 --no-cpu-baseline --no-parity \
+            > "$O/trace.log" 2>&1) || exit 1 ;;
+    collect) step collect 1200 bash scripts/collect_profiles.sh "$TAG" > "$O/collect.log" 2>&1 ;;
+    aux) step aux 300 python -u scripts/aux_bench.py > "$O/aux_bench.json" 2> "$O/aux_bench.err" ;;
+    auxpmc) (cd /tmp && export TMPDIR=/tmp && step auxpmc 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU \
+            SQ_WAVES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d "$O/pmc_aux" -o run -- \
+            python3 "$R/scripts/aux_bench.py" > "$O/pmc_aux.log" 2>&1) || exit 1 ;;
+    host) step host 600 python -u scripts/host_bench.py > "$O/host_bench.json" 2> "$O/host_bench.err" ;;
+    ab) step ab 600 python -u scripts/ab_variants.py ${AB_ARGS:-} > "$O/ab_${AB_NAME:-run}.txt" 2>&1 ;;
+    abg) step abg 600 python -u scripts/ab_gecko_variants.py ${AB_ARGS:-} > "$O/abg_${AB_NAME:-run}.txt" 2>&1 ;;
+    *) echo "unknown step $s"; exit 2 ;;
+  esac
+done
 echo done

@@ -412,3 +412,112 @@ def run_deadline_scenarios(device: int = 0, max_batch: int = 16):
     finally:
         raw.close()
         oa.close()
+
+
+def run_close_race_scenarios(device: int = 0, threads: int = 8, per_writer: int = 1500, run_s: float = 0.4):
+    """Close racing the per-datagram calls (include/hyobfs_conn.h, hyobfs_conn_close):
+    `threads` threads (half writers, half readers) call write_to / read_from in a
+    loop while the main thread closes the connection, in plain and coalescing
+    mode.  Every thread must leave with EBADF (Go: net.ErrClosed) -- never a crash
+    or a use of freed memory (the CPU tier runs this under AddressSanitizer) --
+    every call after close must fail with EBADF, and every datagram a write_to
+    accepted must reach the wire (close sends what the coalescer holds; a write
+    that races close is refused or sent, never dropped)."""
+    import threading
+    import time
+    sink, pump = _udp(), _udp()
+    sink.setsockopt(socket.SOL_SOCKET, socket.SO_RCVBUF, 32 << 20)
+    s_addr = sink.getsockname()
+    ob = SalamanderObfuscator(PSK, device)
+    valid = [ref.obfuscate(PSK, bytes([i]) * (20 + i), bytes([i]) * 8, 28 + i) for i in range(8)]
+    try:
+        for coalescing in (False, True):
+            c = SalamanderPacketConn(_udp(), ob, batch=64)
+            if coalescing:
+                c.set_coalescing(64, 200)
+            c_addr = c.local_addr()
+            stop_pump = threading.Event()
+            accepted = [0] * threads
+            errs = []
+
+            def pumper():   # valid datagrams into the connection for the readers
+                i = 0
+                while not stop_pump.is_set():
+                    try:
+                        pump.sendto(valid[i % len(valid)], c_addr)
+                    except OSError:
+                        pass
+                    i += 1
+                    if i % 64 == 0:
+                        time.sleep(0.001)
+
+            def worker(t):
+                write = t % 2 == 0
+                try:
+                    while True:
+                        if write:
+                            p = bytes([t]) + accepted[t].to_bytes(4, "little") + b"w" * 40
+                            assert c.write_to(p, s_addr) == len(p)
+                            accepted[t] += 1
+                            if accepted[t] >= per_writer:
+                                time.sleep(0.0005)
+                        else:
+                            m, _ = c.read_from()
+                            assert m in [ref.deobfuscate(PSK, v) for v in valid], m
+                except OSError as e:
+                    if e.errno != errno.EBADF:
+                        errs.append((t, repr(e)))
+                        return
+                except BaseException as e:   # noqa: BLE001 -- reported below
+                    errs.append((t, repr(e)))
+                    return
+                # after close: every further call fails the same way
+                for _ in range(3):
+                    try:
+                        c.write_to(b"late", s_addr) if write else c.read_from()
+                        errs.append((t, "call after close succeeded"))
+                    except OSError as e:
+                        if e.errno != errno.EBADF:
+                            errs.append((t, repr(e)))
+
+            pt = threading.Thread(target=pumper)
+            ws = [threading.Thread(target=worker, args=(t,)) for t in range(threads)]
+            pt.start()
+            for w in ws:
+                w.start()
+            time.sleep(run_s)
+            c.close()
+            for w in ws:
+                w.join(30)
+                assert not w.is_alive(), (coalescing, "a thread is still inside a call after close()")
+            stop_pump.set()
+            pt.join(10)
+            assert not errs, (coalescing, errs[:5])
+            # the main thread's calls after close
+            for call in (lambda: c.write_to(b"x", s_addr), lambda: c.read_from(), lambda: c.flush(),
+                         lambda: c.set_read_deadline(None), lambda: c.set_write_deadline(None),
+                         lambda: c.set_coalescing(16, 10), lambda: c.close()):
+                try:
+                    call()
+                    raise AssertionError((coalescing, "call after close succeeded"))
+                except OSError as e:
+                    assert e.errno == errno.EBADF, (coalescing, e)
+            # every accepted datagram is on the wire
+            want = sum(accepted)
+            assert want > 0
+            sink.settimeout(2.0)
+            got = 0
+            while got < want:
+                try:
+                    wire, addr = sink.recvfrom(4096)
+                except TimeoutError:
+                    break
+                assert addr == c_addr
+                assert len(ref.deobfuscate(PSK, wire)) == 45
+                got += 1
+            assert got == want, (coalescing, got, want)
+            del c
+    finally:
+        sink.close()
+        pump.close()
+        ob.close()

@@ -333,6 +333,10 @@ if __name__ == "__main__":
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         from conn_cases import run_lifecycle_scenarios
         run_lifecycle_scenarios(n=args[0], max_batch=args[1])
+    elif which == "closerace":
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        from conn_cases import run_close_race_scenarios
+        run_close_race_scenarios(threads=args[0], per_writer=args[1])
     elif which == "deadline":
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         from conn_cases import run_deadline_scenarios

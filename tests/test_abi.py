@@ -26,8 +26,9 @@ def test_library_exports_every_header_symbol():
 
 def test_abi_basics():
     lib = _lib.load()
-    assert lib.hyobfs_abi_version() == 1
+    assert lib.hyobfs_abi_version() == _lib.ABI_VERSION == 2
     assert _lib.status_string(_lib.HYOBFS_ERR_PSK_TOO_SHORT) == "PSK must be at least 4 bytes"
+    assert _lib.status_string(_lib.HYOBFS_ERR_CLOSED) == "use of closed connection"
     assert lib.hyobfs_batch_workspace_size(0) == 8
     assert lib.hyobfs_batch_workspace_size(257) == 3 * 8
 
@@ -90,3 +91,24 @@ def test_gecko_and_realm_struct_layouts_match_headers(tmp_path):
         header = "hyobfs_realm.h" if ct.startswith("hyobfs_punch") else "hyobfs_gecko.h"
         vals = _c_layout(tmp_path, header, ct, list(dt.names))
         assert vals == [dt.fields[n][1] for n in dt.names] + [dt.itemsize], ct
+
+
+def test_header_abi_version_matches_bindings():
+    """HYOBFS_ABI_VERSION in the header, the library and the Python bindings agree."""
+    import re
+    text = open(os.path.join(ROOT, "include", "hyobfs.h")).read()
+    assert int(re.search(r"#define HYOBFS_ABI_VERSION (\d+)", text).group(1)) == _lib.ABI_VERSION
+    assert int(re.search(r"#define HYOBFS_ERR_CLOSED \((-\d+)\)", text).group(1)) == _lib.HYOBFS_ERR_CLOSED
+
+
+def test_load_refuses_other_abi_version(tmp_path):
+    """_lib.load() refuses a library built for another ABI version (struct layouts and
+    enum values differ between versions, include/hyobfs.h)."""
+    src = tmp_path / "old.c"
+    names = [n for n in _lib.header_functions()]
+    body = "\n".join(f"void {n}(void) {{}}" for n in names if n != "hyobfs_abi_version")
+    src.write_text(body + "\nint hyobfs_abi_version(void) { return 1; }\n")
+    so = tmp_path / "libold.so"
+    subprocess.run(["gcc", "-shared", "-fPIC", str(src), "-o", str(so)], check=True)
+    with pytest.raises(OSError, match="ABI version 1"):
+        _lib.load(str(so))

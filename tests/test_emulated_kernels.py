@@ -37,7 +37,7 @@ SPECS = {
     "test_emulated_packed_auto": lambda p: (p["which"], p["args"], {"HYEMU_CUS": "2"}),
     "test_emulated_tile_kernel": lambda p: (p["which"], p["args"], {"HYOBFS_KERNEL": "tile", "HYEMU_CUS": "2"}),
     "test_emulated_wave_kernel_forced": lambda p: None if p["which"] in ("conn", "host", "coalesce", "quic",
-                                                                         "lifecycle", "deadline") else (
+                                                                         "lifecycle", "deadline", "closerace") else (
         p["which"], p["args"], {"HYEMU_CUS": p["cus"], "HYOBFS_KERNEL": "wave"}),
     "test_emulated_wave_kernel_run_lengths": lambda p: (
         p["which"], p["args"], {"HYOBFS_RUN_LOG2": p["run_log2"], "HYOBFS_KERNEL": "wave"}),
@@ -105,6 +105,7 @@ CASES = [
     ("coalesce", "8 150 4 32", "2"),     # many threads on one coalescing conn (hyobfs_conn_set_coalescing)
     ("lifecycle", "60 16", "2"),         # close() flushes, wakes blocked callers; deferred send errors
     ("deadline", "", "2"),               # Set{Read,Write}Deadline, both modes
+    ("closerace", "8 1500", "2"),        # 8 threads in read_from / write_to while close() runs, under ASan
     ("far", "200 300 15 1", "8"),        # workgroup bases beyond 2^31
     ("far", "200 300 15 0", "8"),
     ("gecko", "40 7", "2"),              # Gecko frame encode + parse kernels (gecko.hip), aligned sweep
@@ -154,16 +155,7 @@ def test_emulated_packed_auto(emu_lib, which, args):
 # salt-word position of the PSK (lengths 4..127, including the two-block case
 # 121..127), and layouts that do not qualify (odd lengths, inputs over 4 KiB: the
 # wave kernel).
-TILE_CASES = [
-    ("uniform", "257 1200 1"), ("uniform", "256 1200 0"), ("uniform", "301 1192 1"), ("uniform", "301 1192 0"),
-    ("uniform", "33 16 1"), ("uniform", "33 24 0"), ("uniform", "300 17 1"), ("uniform", "99 1201 0"),
-    ("slotted", "70 1200 1 24 8 16"), ("slotted", "70 1208 0 8 0 16"), ("slotted", "45 2040 1 0 16 9"),
-    ("slotted", "37 4096 0 16 0 31"), ("slotted", "21 9000 1 0 0 16"), ("slotted", "40 64 1 0 0 4"),
-    ("slotted", "40 64 0 0 24 5"), ("slotted", "23 100 1 4 4 16"), ("slotted", "30 1216 0 0 0 16"),
-    ("slotted", "17 4096 1 8 0 16"), ("slotted", "17 4104 1 0 0 16"),
-] + [("slotted", f"18 {L} 1 {pad} 0 {k}") for k, L, pad in
-     [(4, 40, 0), (8, 48, 8), (12, 136, 0), (20, 200, 16), (60, 96, 0), (100, 1000, 8), (119, 512, 0),
-      (120, 256, 0), (121, 256, 8), (124, 512, 0), (127, 264, 0), (128, 64, 0), (300, 1200, 0)]]
+from tile_cases import TILE_CASES  # noqa: E402  (the tile kernel's layout grid, shared with the GPU tier)
 
 
 @pytest.mark.parametrize("which,args", TILE_CASES)
@@ -206,7 +198,7 @@ def test_emulated_wave_kernel_packed_run_lengths(emu_lib, which, args, run_log2)
 @pytest.mark.parametrize("which,args,cus", CASES)
 def test_emulated_wave_kernel_forced(emu_lib, which, args, cus):
     """The wave-group kernel (HYOBFS_KERNEL=wave) on every case, also where AUTO runs the tile kernel."""
-    if which in ("conn", "host", "coalesce", "quic", "lifecycle", "deadline"):
+    if which in ("conn", "host", "coalesce", "quic", "lifecycle", "deadline", "closerace"):
         pytest.skip("kernel-independent host paths run once, under the default kernel")
     _run(emu_lib, which, args, {"HYEMU_CUS": cus, "HYOBFS_KERNEL": "wave"})
 

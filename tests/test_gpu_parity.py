@@ -420,6 +420,56 @@ def test_ragged_layouts_vs_oracle(obfs, gpu, coracle, obf, layout):
     assert (got[~written] == sentinel).all()
 
 
+# ------------------------------------------------------- the tile kernel's grid
+from tile_cases import TILE_CASES, expects_tile, slotted_params  # noqa: E402
+
+
+@pytest.mark.parametrize("kernel", ["auto", "wave"])
+@pytest.mark.parametrize("which,args", TILE_CASES)
+def test_tile_layout_grid(gpu, coracle, which, args, kernel):
+    """The tile kernel's layout grid on the GPU (tests/tile_cases.py, the same cases the
+    CPU tier emulates): gapped and 0-mod-16 slots, 4096-byte input strides (64 KiB of
+    staged LDS), the 8-byte input tail, multi-pass compose (9000-byte slots), every salt
+    word 0..15 including the two-block PSKs, and layouts that fall back to the wave
+    kernel.  Byte for byte against the C oracle, sentinel bytes in every gap, the kernel
+    AUTO chose checked (hyobfs_salamander_batch_kernel); "wave" runs the same case on
+    the wave kernel."""
+    import torch
+    import hysteria_amd
+    n, L, obf, slot_pad, in_pad, psk = slotted_params(which, args)
+    W = L + 8 if obf else L - 8
+    S, istride = W + slot_pad, L + in_pad
+    inp = np.frombuffer(ref.stream_bytes(1, 0, n * istride + 16), np.uint8).copy()
+    salts = ref.splitmix64_array(2, 0, n)
+    cap = n * S
+    exp, eoff, elen, etot = coracle.batch(obf, psk, n, inp, in_stride=istride, len_uniform=L,
+                                          salts=salts if obf else None, out_cap=cap, out_stride=S)
+    sentinel = 0xA5
+    out = torch.full((cap + 64,), sentinel, dtype=torch.uint8, device=gpu)
+    out_off = torch.zeros(n, dtype=torch.int64, device=gpu)
+    out_len = torch.zeros(n, dtype=torch.int32, device=gpu)
+    total = torch.zeros(1, dtype=torch.int64, device=gpu)
+    with hysteria_amd.SalamanderObfuscator(psk, 0) as o:
+        o.set_kernel(kernel)
+        d_in = _dev(inp, gpu)
+        kw = dict(inp=d_in, n=n, in_stride=istride, len_uniform=L, out=out, out_cap=cap, out_stride=S,
+                  out_off=out_off, out_len=out_len, out_total=total)
+        if obf:
+            kw["salts"] = _u64(salts, gpu)
+        want = "tile" if kernel == "auto" and expects_tile(n, L, obf, slot_pad, in_pad) else "wave"
+        assert o.batch_kernel(obf, **kw) == want, (which, args)
+        (o.obfuscate_batch if obf else o.deobfuscate_batch)(**kw)
+        got = _host(out)
+    assert np.array_equal(_host(out_off).view(np.uint64), eoff)
+    assert np.array_equal(_host(out_len).view(np.uint32), elen)
+    assert int(_host(total)[0]) == etot
+    written = np.zeros(cap + 64, bool)
+    for off, w in zip(eoff, elen):
+        written[int(off):int(off) + int(w)] = True
+    assert np.array_equal(got[written], exp[:cap][written[:cap]])
+    assert (got[~written] == sentinel).all(), "bytes outside the regions were written"
+
+
 def test_empty_batch(obfs, gpu):
     import torch
     out = torch.zeros(16, dtype=torch.uint8, device=gpu)
@@ -591,6 +641,14 @@ def test_packet_conn_deadlines(gpu):
     sys.path.insert(0, os.path.dirname(__file__))
     from conn_cases import run_deadline_scenarios
     run_deadline_scenarios(device=0)
+
+
+def test_packet_conn_close_race(gpu):
+    """Close racing 8 threads in read_from / write_to, plain and coalescing mode: every
+    thread leaves with EBADF, every later call fails with EBADF, every accepted
+    datagram reaches the wire (include/hyobfs_conn.h, hyobfs_conn_close)."""
+    from conn_cases import run_close_race_scenarios
+    run_close_race_scenarios(device=0, threads=8, per_writer=1500)
 
 
 def test_packet_conn_coalescing_loopback(gpu):
