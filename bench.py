@@ -47,9 +47,9 @@ KERNEL_NAMES = {
     "uniform": {"auto": "salamander_tile_kernel<obfuscate> (salamander_tile.h)",
                 "tile": "salamander_tile_kernel<obfuscate> (salamander_tile.h)",
                 "wave": "salamander_wave_kernel<obfuscate, slotted> (salamander_wave.h)"},
-    "bimodal": {"auto": "salamander_wave_kernel<obfuscate, packed> (salamander_wave.h) + tile-sum scan",
-                "tile": "salamander_wave_kernel<obfuscate, packed> (salamander_wave.h) + tile-sum scan",
-                "wave": "salamander_wave_kernel<obfuscate, packed> (salamander_wave.h) + tile-sum scan"},
+    "bimodal": {"auto": "salamander_stream_kernel<obfuscate> (salamander_stream.h) + 3 prepass launches",
+                "tile": "salamander_stream_kernel<obfuscate> (salamander_stream.h) + 3 prepass launches",
+                "wave": "salamander_wave_kernel<obfuscate, packed> (salamander_wave.h) + offset prepass + tile-sum scan"},
 }
 
 
@@ -193,11 +193,12 @@ def setup_uniform(hy, obfs, dev, P, L, first):
 
 
 def setup_bimodal(hy, obfs, dev, P, first):
+    """configs[2]: the datagrams back to back in one buffer (contiguous input: in_off
+    NULL, in_stride 0, include/hyobfs.h), packed output; the wire, contiguous too, is
+    the deobfuscate step's input."""
     import torch
     lens = torch.empty(P, dtype=torch.int32, device=dev)
     hy.synth_bimodal_lengths(lens, P, 3, first)
-    in_off = torch.zeros(P, dtype=torch.int64, device=dev)
-    in_off[1:] = torch.cumsum(lens[:-1].to(torch.int64), 0)
     total_in = int(lens.to(torch.int64).sum())
     inp = torch.empty(total_in + 16, dtype=torch.uint8, device=dev)
     # stream offset of this rank's shard (global packed input): the lengths of
@@ -219,14 +220,16 @@ def setup_bimodal(hy, obfs, dev, P, first):
     out_off = torch.empty(P, dtype=torch.int64, device=dev)
     out_len = torch.empty(P, dtype=torch.int32, device=dev)
     back = torch.empty(total_in + 16, dtype=torch.uint8, device=dev)
-    ws = torch.empty(hy.workspace_size(P), dtype=torch.uint8, device=dev)
+    nws = max(obfs.workspace_bytes(inp=inp, n=P, in_len=lens, out=wire, out_cap=cap),
+              obfs.workspace_bytes(inp=wire, n=P, in_len=out_len, out=back, out_cap=total_in))
+    ws = torch.empty(max(nws, 16), dtype=torch.uint8, device=dev)
 
     def step_obf():
-        obfs.obfuscate_batch(inp, P, in_off=in_off, in_len=lens, salts=salts, out=wire, out_cap=cap,
+        obfs.obfuscate_batch(inp, P, in_len=lens, salts=salts, out=wire, out_cap=cap,
                              out_off=out_off, out_len=out_len, workspace=ws, workspace_bytes=ws.numel())
 
     def step_deobf():
-        obfs.deobfuscate_batch(wire, P, in_off=out_off, in_len=out_len, out=back, out_cap=total_in,
+        obfs.deobfuscate_batch(wire, P, in_len=out_len, out=back, out_cap=total_in,
                                workspace=ws, workspace_bytes=ws.numel())
 
     return dict(obf=step_obf, deobf=step_deobf, payload=total_in, obf_bytes=2 * total_in + 16 * P,
@@ -332,7 +335,7 @@ def main():
         P = args.packets_per_gpu or (1 << 22)
         first, P = weak_shard(P, rank)
         w = setup_bimodal(hy, obfs, dev, P, first)
-        config = {"workload": f"bimodal 40% 64 B / 60% 1350 B, {P} datagrams per GPU, packed output",
+        config = {"workload": f"bimodal 40% 64 B / 60% 1350 B, {P} datagrams per GPU, contiguous input, packed output",
                   "datagrams_per_gpu": P, "global_datagrams": P * world, "psk": PSK.decode(),
                   "parallelism": f"packet-index shards x{world}"}
     torch.cuda.synchronize()
@@ -376,7 +379,8 @@ def main():
         mb = measure(wb, "bimodal")
         torch.cuda.synchronize()
         rt = bool(torch.equal(wb["back"][:wb["payload"]], wb["inp"][:wb["payload"]]))
-        res["bimodal"] = {"workload": "configs[2]: 4194304 datagrams, 40% 64 B / 60% 1350 B, packed output",
+        res["bimodal"] = {"workload": "configs[2]: 4194304 datagrams, 40% 64 B / 60% 1350 B, contiguous input, "
+                                      "packed output",
                           "value": round(mb["value"], 2), "unit": "GiB/s", "ms_per_step": round(mb["ms"], 4),
                           "roofline": mb["roofline"], "deobfuscate": mb["deobfuscate"],
                           "parity": {"roundtrip_identity": rt}}

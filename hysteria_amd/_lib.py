@@ -109,6 +109,7 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         "hyobfs_salamander_obfuscate_auto": (sz, [pctx, vp, sz, vp, sz]),
         "hyobfs_salamander_deobfuscate": (sz, [pctx, vp, sz, vp, sz]),
         "hyobfs_batch_workspace_size": (u64, [u64]),
+        "hyobfs_batch_workspace_bytes": (u64, [ctypes.POINTER(HyobfsBatch)]),
         "hyobfs_salamander_batch_kernel": (i32, [pctx, ctypes.POINTER(HyobfsBatch), i32]),
         "hyobfs_salamander_obfuscate_batch": (i32, [pctx, ctypes.POINTER(HyobfsBatch), vp]),
         "hyobfs_salamander_deobfuscate_batch": (i32, [pctx, ctypes.POINTER(HyobfsBatch), vp]),

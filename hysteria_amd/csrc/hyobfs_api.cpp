@@ -274,9 +274,12 @@ int fill_params(hyobfs_salamander* c, const hyobfs_batch* b, bool obf, BatchPara
     bp.out_len = b->out_len;
     bp.out_total = reinterpret_cast<unsigned long long*>(b->out_total);
     bp.kernel = c->kernel;
-    if (b->n && b->out_stride == 0 && b->workspace) {   // packed: caller's tile-sum scratch
-        if (b->workspace_bytes < hyobfs_batch_workspace_size(b->n)) return HYOBFS_ERR_INVALID;
-        bp.tile_sums = static_cast<uint64_t*>(b->workspace);
+    // device scratch: the caller's workspace, or (run_batch) the context's pool
+    const uint64_t need = hyobfs::batch_workspace_bytes(obf, bp);
+    if (need && b->workspace) {
+        if (b->workspace_bytes < need) return HYOBFS_ERR_INVALID;
+        bp.scratch = b->workspace;
+        bp.tile_sums = static_cast<uint64_t*>(b->workspace);   // (packed, explicit offsets: the tile sums)
     }
     return HYOBFS_OK;
 }
@@ -299,11 +302,12 @@ int run_batch(hyobfs_salamander* c, const hyobfs_batch* b, void* stream, bool ob
     const int rc = validate_and_fill(c, b, obf, bp, s);
     if (rc != HYOBFS_OK) return rc;
     void* scratch = nullptr;
-    if (b->n && b->out_stride == 0 && !b->workspace) {   // packed, no caller workspace: the context's pool
+    const uint64_t need = hyobfs::batch_workspace_bytes(obf, bp);
+    if (need && !b->workspace) {   // no caller workspace: the context's pool
         hipMemPool_t pool = scratch_pool(c);
         if (!pool) return HYOBFS_ERR_HIP;
-        if (hipMallocFromPoolAsync(&scratch, hyobfs_batch_workspace_size(b->n), pool, s) != hipSuccess)
-            return HYOBFS_ERR_NOMEM;
+        if (hipMallocFromPoolAsync(&scratch, need, pool, s) != hipSuccess) return HYOBFS_ERR_NOMEM;
+        bp.scratch = scratch;
         bp.tile_sums = static_cast<uint64_t*>(scratch);
     }
     const hipError_t e = hyobfs::launch_salamander(obf, bp, c->kp, s);
@@ -606,6 +610,25 @@ size_t hyobfs_salamander_deobfuscate(hyobfs_salamander* c, const uint8_t* in, si
     if (in_len > hyobfs::kMaxDatagram) return 0;
     std::lock_guard<std::mutex> lk(c->mu);
     return run_one(c, false, in, in_len, nullptr, out, W);
+}
+
+uint64_t hyobfs_batch_workspace_bytes(const hyobfs_batch* b) {
+    if (!b) return 0;
+    hyobfs::BatchParams bp{};
+    bp.n = b->n;
+    bp.in = b->in;
+    bp.in_off = b->in_off;
+    bp.in_stride = b->in_stride;
+    bp.in_len = b->in_len;
+    bp.out_cap = b->out_cap;
+    bp.out_stride = b->out_stride;
+    // the larger of the stream kernel's and the fallback's needs: independent of the
+    // context's kernel choice
+    bp.kernel = hyobfs::kKernelAuto;
+    const uint64_t a = hyobfs::batch_workspace_bytes(true, bp);
+    bp.kernel = hyobfs::kKernelWave;
+    const uint64_t w = hyobfs::batch_workspace_bytes(true, bp);
+    return a > w ? a : w;
 }
 
 uint64_t hyobfs_batch_workspace_size(uint64_t n) {

@@ -32,7 +32,7 @@ constexpr int kTile = 256;          // datagrams per tile-sum entry of the packe
 constexpr uint32_t kMaxDatagram = (1u << 24) - 64;  // longest datagram a batch accepts
 constexpr uint64_t kMaxStride = 1ull << 24;         // longest slot of a slotted output
 // batch kernels (include/hyobfs.h HYOBFS_KERNEL_*)
-constexpr int kKernelAuto = 0, kKernelWave = 1, kKernelTile = 2;
+constexpr int kKernelAuto = 0, kKernelWave = 1, kKernelTile = 2, kKernelStream = 3;
 
 // BLAKE2b state for the per-packet key, precomputed on the host from the PSK
 // alone (salamander.go:88-91 hashes PSK || salt; every block before the one
@@ -64,6 +64,7 @@ struct BatchParams {
     unsigned long long* out_total;
     const uint64_t* tile_prefix;  // packed: exclusive prefix of tile sums (ntiles+1)
     uint64_t* tile_sums;          // packed: scratch, ntiles+1 entries
+    void* scratch;                // contiguous input: the stream prepass's scratch (batch_workspace_bytes)
     uint32_t run_log2;            // wave kernel: datagrams per run = 2^run_log2
     uint64_t blk0 = 0;            // wave kernel, packed runs of 64: first workgroup of this launch
     int kernel;                   // HYOBFS_KERNEL_* of the context (0 = auto)
@@ -73,8 +74,14 @@ struct BatchParams {
 // HYOBFS_KERNEL environment variable, else 0)
 int resolve_kernel(int ctx_kernel);
 hipError_t launch_salamander(bool obfuscate, const BatchParams& b, const KeyParams& k, hipStream_t s);
-// the kernel launch_salamander would run (kKernelTile / kKernelWave; kKernelAuto for an empty batch)
+// the kernel launch_salamander would run (kKernelTile / kKernelWave / kKernelStream;
+// kKernelAuto for an empty batch)
 int batch_kernel(bool obfuscate, const BatchParams& b);
+// device scratch a launch of this batch needs (0: none); launch_salamander takes it
+// from b.tile_sums / b.scratch as laid out by batch_workspace_layout
+uint64_t batch_workspace_bytes(bool obfuscate, const BatchParams& b);
+// contiguous input: datagram i at in + in_len[0] + ... + in_len[i-1]
+inline bool contiguous_input(const BatchParams& b) { return !b.in_off && b.in_stride == 0 && b.in_len && b.n > 1; }
 hipError_t launch_keys(const KeyParams& k, const uint64_t* salts, uint8_t* keys, uint64_t n,
                        hipStream_t s);
 hipError_t launch_gecko_encode(const KeyParams& k, const hyobfs_gecko_batch& b, hipStream_t s);

@@ -13,7 +13,7 @@
 //     One-shot workgroups of 16 datagrams: a key wave beside three data waves.
 //   * salamander_wave_kernel (salamander_wave.h): every other layout (packed
 //     output, ragged lengths, any alignment).  One wave per 64-datagram group.
-#include "salamander_tile.h"
+#include "salamander_stream.h"
 
 namespace hyobfs {
 
@@ -26,7 +26,11 @@ namespace hyobfs {
     extern template void launch_tile_sw<true, n>(const BatchParams&, const KeyParams&, const TileParams&,   \
                                                  hipStream_t);                                              \
     extern template void launch_tile_sw<false, n>(const BatchParams&, const KeyParams&, const TileParams&,  \
-                                                  hipStream_t);
+                                                  hipStream_t);                                             \
+    extern template void launch_stream_sw<true, n>(const BatchParams&, const KeyParams&, const StreamParams&, \
+                                                   hipStream_t);                                            \
+    extern template void launch_stream_sw<false, n>(const BatchParams&, const KeyParams&, const StreamParams&, \
+                                                    hipStream_t);
 HY_EXTERN_SW(0) HY_EXTERN_SW(1) HY_EXTERN_SW(2) HY_EXTERN_SW(3) HY_EXTERN_SW(4) HY_EXTERN_SW(5)
 HY_EXTERN_SW(6) HY_EXTERN_SW(7) HY_EXTERN_SW(8) HY_EXTERN_SW(9) HY_EXTERN_SW(10) HY_EXTERN_SW(11)
 HY_EXTERN_SW(12) HY_EXTERN_SW(13) HY_EXTERN_SW(14) HY_EXTERN_SW(15)
@@ -185,13 +189,62 @@ static void launch_main(const BatchParams& bp, const KeyParams& k, hipStream_t s
     }
 }
 
+// Contiguous input, packed output: the stream kernel (salamander_stream.h) unless the
+// wave kernel is forced or the input is not 16-byte aligned (LDS-DMA moves 16-byte
+// chunks); then the stream prepass writes the input offsets and the kernels for
+// explicit offsets run on them.
+static bool stream_eligible(const BatchParams& b) {
+    return contiguous_input(b) && b.out_stride == 0 && resolve_kernel(b.kernel) != kKernelWave &&
+           (reinterpret_cast<uintptr_t>(b.in) & 15u) == 0;
+}
+
+static uint64_t align16(uint64_t x) { return (x + 15) & ~15ull; }
+
+uint64_t batch_workspace_bytes(bool obf, const BatchParams& b) {
+    (void)obf;
+    if (b.n == 0) return 0;
+    const uint64_t tsums = (div_up(b.n, kTile) + 1) * 8;
+    if (!contiguous_input(b)) return b.out_stride == 0 ? tsums : 0;
+    if (stream_eligible(b)) return stream_workspace_bytes(b.n, b.out_cap, true, false);
+    return align16(stream_workspace_bytes(b.n, 0, false, true)) + (b.out_stride == 0 ? tsums : 0);
+}
+
 // Which kernel launch_salamander runs for this batch (HYOBFS_KERNEL_*; no launch).
 int batch_kernel(bool obf, const BatchParams& b) {
     if (b.n == 0) return kKernelAuto;   // nothing runs
+    if (stream_eligible(b)) return kKernelStream;
     TileParams T;
-    const bool tile = b.out_stride != 0 && resolve_kernel(b.kernel) != kKernelWave &&
-                      (obf ? tile_params<true>(b, T) : tile_params<false>(b, T));
+    BatchParams bp = b;
+    if (contiguous_input(b)) bp.in_off = reinterpret_cast<const uint64_t*>(16);   // offsets from the prepass
+    const bool tile = bp.out_stride != 0 && resolve_kernel(bp.kernel) != kKernelWave &&
+                      (obf ? tile_params<true>(bp, T) : tile_params<false>(bp, T));
     return tile ? kKernelTile : kKernelWave;
+}
+
+template <bool OBF>
+static hipError_t launch_contiguous(BatchParams& bp, const KeyParams& k, hipStream_t s, bool& done) {
+    done = false;
+    if (!bp.scratch) return hipErrorInvalidValue;
+    StreamParams S;
+    if (stream_eligible(bp)) {
+        launch_stream_prepass<OBF>(bp, S, bp.scratch, true, false, s);
+        switch (k.salt_pos >> 3) {
+#define HY_CASE(n) \
+    case n: launch_stream_sw<OBF, n>(bp, k, S, s); break;
+            HY_CASE(0) HY_CASE(1) HY_CASE(2) HY_CASE(3) HY_CASE(4) HY_CASE(5) HY_CASE(6) HY_CASE(7)
+            HY_CASE(8) HY_CASE(9) HY_CASE(10) HY_CASE(11) HY_CASE(12) HY_CASE(13) HY_CASE(14)
+            HY_CASE(15)
+#undef HY_CASE
+        }
+        done = true;
+        return hipGetLastError();
+    }
+    launch_stream_prepass<OBF>(bp, S, bp.scratch, false, true, s);
+    bp.in_off = S.in_off_out;
+    if (bp.out_stride == 0)
+        bp.tile_sums = reinterpret_cast<uint64_t*>(static_cast<uint8_t*>(bp.scratch) +
+                                                   align16(stream_workspace_bytes(bp.n, 0, false, true)));
+    return hipGetLastError();
 }
 
 hipError_t launch_salamander(bool obf, const BatchParams& b, const KeyParams& k, hipStream_t s) {
@@ -200,7 +253,13 @@ hipError_t launch_salamander(bool obf, const BatchParams& b, const KeyParams& k,
     if (ntiles > 0x7fffffffull) return hipErrorInvalidValue;
     if (k.nblk == 2 && (k.salt_pos >> 3) != 15) return hipErrorInvalidValue;   // by construction
     BatchParams bp = b;
-    if (b.out_stride == 0) {
+    if (contiguous_input(b)) {
+        bool done = false;
+        const hipError_t e = obf ? launch_contiguous<true>(bp, k, s, done) : launch_contiguous<false>(bp, k, s, done);
+        if (e != hipSuccess || done) return e;
+    }
+    if (bp.out_stride == 0) {
+        if (!bp.tile_sums) return hipErrorInvalidValue;
         const dim3 grid((uint32_t)ntiles), block(kTile);
         if (obf)
             hipLaunchKernelGGL(tile_sums_kernel<true>, grid, block, 0, s, bp);

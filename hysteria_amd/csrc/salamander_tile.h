@@ -234,6 +234,23 @@ __device__ __forceinline__ void store16_global(uint8_t* p, uint64_t lo, uint64_t
 #endif
 }
 
+// The wire salt the key wave reads while the DMA waves stage the same line
+// (deobfuscate).  HY_TILE_WIRE_SALT 0: non-temporal load; 1: temporal load, so the
+// line is allocated in L2 and the DMA's request for it can hit there.
+#ifndef HY_TILE_WIRE_SALT
+#define HY_TILE_WIRE_SALT 0
+#endif
+__device__ __forceinline__ uint64_t load8_wire_salt(const uint8_t* p) {   // 8-aligned
+#if HY_TILE_WIRE_SALT == 0 || defined(HYOBFS_EMULATE)
+    return load8_nt(p);
+#else
+    typedef uint32_t v2u __attribute__((ext_vector_type(2)));
+    typedef const __attribute__((address_space(1))) v2u gv2u;
+    const v2u v = *(gv2u*)(p);
+    return (uint64_t)v.y << 32 | v.x;
+#endif
+}
+
 __device__ __forceinline__ void glds16(const uint8_t* g, uint8_t* l) {   // LDS-DMA: l = wave base + lane * 16
 #ifdef HYOBFS_EMULATE
     std::memcpy(l + 16 * (threadIdx.x & 63), g, 16);
@@ -270,7 +287,7 @@ __global__ __launch_bounds__(256, HY_TILE_MIN_WAVES) void salamander_tile_kernel
         // ---- the key wave: salts, BLAKE2b-256 on quads (lane 4k+i: word i of key k), LDS
         const uint32_t qk = lane >> 2, qi = lane & 3;
         uint64_t salt = 0;
-        if (qk < nt) salt = OBF ? B.salts[p0 + qk] : load8_nt(ib + qk * in_stride);
+        if (qk < nt) salt = OBF ? B.salts[p0 + qk] : load8_wire_salt(ib + qk * in_stride);
         const uint64_t kw = quad_key<SW>(K, salt, qi);
         if (qk < nt) {
             s_key[qk * 8 + qi] = kw;

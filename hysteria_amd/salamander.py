@@ -142,6 +142,7 @@ class SalamanderObfuscator:
         """Batch kernel of this context: "auto" (the tile kernel where it applies, else the
         wave-group kernel), "wave" (forced) or "tile" (include/hyobfs.h, HYOBFS_KERNEL_*)."""
         check(self._lib.hyobfs_salamander_set_kernel(self._h, self.KERNELS[kernel]), "set_kernel")
+        self.kernel = kernel
 
     # ------------------------------------------------------------ salt source
     def seed(self, seed: int) -> None:
@@ -198,7 +199,14 @@ class SalamanderObfuscator:
         b = _make_batch(inp=inp, n=n, out=out, **kw)
         k = self._lib.hyobfs_salamander_batch_kernel(self._h, ctypes.byref(b), int(bool(obf)))
         check(min(k, 0), "batch_kernel")
-        return {0: "none", 1: "wave", 2: "tile"}[k]
+        return {0: "none", 1: "wave", 2: "tile", 3: "stream"}[k]
+
+    @staticmethod
+    def workspace_bytes(*, inp, n, out, **kw) -> int:
+        """hyobfs_batch_workspace_bytes: the device scratch a batch call with these
+        arguments needs under any kernel choice (0: none)."""
+        b = _make_batch(inp=inp, n=n, out=out, **kw)
+        return int(_lib.load().hyobfs_batch_workspace_bytes(ctypes.byref(b)))
 
     def obfuscate_batch(self, inp, n, *, salts, out, **kw) -> None:
         """Obfuscate n datagrams on the device (layout rules: include/hyobfs.h).

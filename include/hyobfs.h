@@ -119,7 +119,8 @@ int hyobfs_salamander_device(const hyobfs_salamander* ctx);
 enum {
     HYOBFS_KERNEL_AUTO = 0,
     HYOBFS_KERNEL_WAVE = 1,
-    HYOBFS_KERNEL_TILE = 2
+    HYOBFS_KERNEL_TILE = 2,
+    HYOBFS_KERNEL_STREAM = 3   /* reported by hyobfs_salamander_batch_kernel only */
 };
 int hyobfs_salamander_set_kernel(hyobfs_salamander* ctx, int kernel);
 
@@ -156,6 +157,9 @@ size_t hyobfs_salamander_deobfuscate(hyobfs_salamander* ctx, const uint8_t* in,
  *
  *   input   : len  L_i = in_len ? in_len[i] : len_uniform
  *             bytes at in + (in_off ? in_off[i] : i * in_stride)       (any alignment)
+ *             CONTIGUOUS input: in_off == NULL, in_stride == 0 and in_len != NULL
+ *             put datagram i at in + L_0 + ... + L_{i-1} (back to back; a
+ *             16-byte aligned `in` lets packed output run the stream kernel)
  *   salt    : obfuscate only: salts[i], 8 bytes, little-endian u64
  *             (salt byte b = (salts[i] >> 8b) & 0xff)
  *   output  : W_i = L_i + 8 (obfuscate) or L_i - 8 (deobfuscate)
@@ -174,8 +178,9 @@ size_t hyobfs_salamander_deobfuscate(hyobfs_salamander* ctx, const uint8_t* in,
  *
  * `out` must be 16-byte aligned.  All pointers are device-accessible; the
  * call only enqueues work on `stream` (a hipStream_t; NULL = the HIP null
- * stream, as everywhere in HIP) and returns.  workspace (packed layout only):
- * device scratch of at least hyobfs_batch_workspace_size(n) bytes, or NULL:
+ * stream, as everywhere in HIP) and returns.  workspace: device scratch of at
+ * least hyobfs_batch_workspace_bytes(b) bytes (0 for slotted batches with
+ * explicit offsets; hyobfs_batch_workspace_size(n) for packed ones), or NULL:
  * then the scratch is allocated stream-ordered from a context-owned memory pool
  * and freed behind the launch on the same stream (any number of caller streams
  * and threads; the pool keeps at most 32 MiB cached between calls).
@@ -199,9 +204,15 @@ typedef struct hyobfs_batch {
     uint64_t workspace_bytes;
 } hyobfs_batch;
 
+/* Scratch of a packed batch with explicit or strided input offsets: (ceil(n/256)+1) x 8. */
 uint64_t hyobfs_batch_workspace_size(uint64_t n);
+/* Scratch any batch needs, whatever the kernel choice: the above for packed
+   batches with explicit offsets; for contiguous input the stream prepass's
+   block sums (16 B per 1024 datagrams), tile descriptors (32 B per 16 KiB of
+   out_cap) or input offsets (8 B per datagram); 0 for slotted batches. */
+uint64_t hyobfs_batch_workspace_bytes(const hyobfs_batch* b);
 /* Which batch kernel a call with this batch would run under the context's
-   setting (HYOBFS_KERNEL_TILE or HYOBFS_KERNEL_WAVE; HYOBFS_KERNEL_AUTO for an
+   setting (HYOBFS_KERNEL_TILE, _WAVE or _STREAM; HYOBFS_KERNEL_AUTO for an
    empty batch), or a negative status for an invalid batch.  No device work:
    tests use it to prove which kernel their case exercised. */
 int hyobfs_salamander_batch_kernel(hyobfs_salamander* ctx, const hyobfs_batch* b, int obfuscate);

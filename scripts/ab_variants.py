@@ -8,7 +8,9 @@ streaming kernel by up to +-5 % between processes, is shared.
 
 A name ending in "!" is an ablation build (wrong output): its wire is not checked.
 AB_WORKLOAD=bimodal runs BASELINE configs[2] instead (P datagrams of the 40 % 64 B /
-60 % 1350 B mix, default 4M, packed output).
+60 % 1350 B mix, default 4M, packed output).  Bimodal input is contiguous (in_off NULL:
+the stream kernel under auto); a kernel name with "@off" passes explicit in_off /
+out_off arrays instead (the round-3 layout: the wave kernel).
 """
 import os
 import statistics
@@ -44,7 +46,10 @@ if WL == "bimodal":
     out_off = torch.empty(P, dtype=torch.int64, device=dev)
     out_len = torch.empty(P, dtype=torch.int32, device=dev)
     back = torch.empty(total_in + 16, dtype=torch.uint8, device=dev)
-    ws = torch.empty(hysteria_amd.workspace_size(P), dtype=torch.uint8, device=dev)
+    SO = hysteria_amd.SalamanderObfuscator
+    nws = max(hysteria_amd.workspace_size(P), SO.workspace_bytes(inp=inp, n=P, in_len=lens, out=wire, out_cap=cap),
+              SO.workspace_bytes(inp=wire, n=P, in_len=out_len, out=back, out_cap=total_in))
+    ws = torch.empty(nws, dtype=torch.uint8, device=dev)
     obf_bytes, deobf_bytes = 2 * total_in + 16 * P, 2 * total_in + 8 * P
     PL = total_in
 else:
@@ -60,21 +65,24 @@ ctxs = {}
 for name, path in libs:
     for k in kernels:
         o = hysteria_amd.SalamanderObfuscator(b"average_password", 0, lib_path=os.path.abspath(path))
-        o.set_kernel(k)
+        o.set_kernel(k.split("@")[0])
+        o.ab_offsets = k.endswith("@off")
         ctxs[f"{name}/{k}"] = (o, name.endswith("!"))
 
 
 def ob(o):
     if WL == "bimodal":
-        return lambda: o.obfuscate_batch(inp, P, in_off=in_off, in_len=lens, salts=salts, out=wire, out_cap=cap,
-                                         out_off=out_off, out_len=out_len, workspace=ws, workspace_bytes=ws.numel())
+        off = dict(in_off=in_off) if o.ab_offsets else {}
+        return lambda: o.obfuscate_batch(inp, P, in_len=lens, salts=salts, out=wire, out_cap=cap, out_off=out_off,
+                                         out_len=out_len, workspace=ws, workspace_bytes=ws.numel(), **off)
     return lambda: o.obfuscate_batch(inp, P, in_stride=L, len_uniform=L, salts=salts, out=wire, out_stride=L + 8)
 
 
 def de(o):
     if WL == "bimodal":
-        return lambda: o.deobfuscate_batch(wire, P, in_off=out_off, in_len=out_len, out=back, out_cap=total_in,
-                                           workspace=ws, workspace_bytes=ws.numel())
+        off = dict(in_off=out_off) if o.ab_offsets else {}
+        return lambda: o.deobfuscate_batch(wire, P, in_len=out_len, out=back, out_cap=total_in,
+                                           workspace=ws, workspace_bytes=ws.numel(), **off)
     return lambda: o.deobfuscate_batch(wire, P, in_stride=L + 8, len_uniform=L + 8, out=back, out_stride=L)
 
 

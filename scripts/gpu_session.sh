@@ -14,6 +14,8 @@
 #   aux             (f)-row rates (scripts/aux_bench.py)
 #   auxpmc          VALU counters of the (f)-row kernels
 #   host            host-to-host rates (scripts/host_bench.py)
+#   pmc:LIB:WL:CTR  one rocprofv3 --pmc pass (counter CTR) of scripts/prof_one.py WL with the
+#                   library main or build_variants/libhyobfs_LIB.so
 #   ab              in-process A/B of library builds (scripts/ab_variants.py; AB_* env vars)
 #   abg             the same for Gecko builds (scripts/ab_gecko_variants.py)
 set -u
@@ -48,6 +50,12 @@ for s in "$@"; do
             SQ_WAVES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d "$O/pmc_aux" -o run -- \
             python3 "$R/scripts/aux_bench.py" > "$O/pmc_aux.log" 2>&1) || exit 1 ;;
     host) step host 600 python -u scripts/host_bench.py > "$O/host_bench.json" 2> "$O/host_bench.err" ;;
+    pmc:*) IFS=: read -r _ LIBN WL CTR <<< "$s"
+            LIBP=$R/hysteria_amd/libhyobfs.so
+            [ "$LIBN" = main ] || LIBP=$R/build_variants/libhyobfs_$LIBN.so
+            (cd /tmp && export TMPDIR=/tmp && export HYOBFS_LIB=$LIBP && step "pmc $LIBN $WL $CTR" 240 rocprofv3 \
+              --pmc $CTR --kernel-trace --output-format csv -d "$O/pmc_${LIBN}_${WL}_$CTR" -o run -- \
+              python3 "$R/scripts/prof_one.py" "$WL" 5 > "$O/pmc_${LIBN}_${WL}_$CTR.log" 2>&1) || exit 1 ;;
     ab) step ab 600 python -u scripts/ab_variants.py ${AB_ARGS:-} > "$O/ab_${AB_NAME:-run}.txt" 2>&1 ;;
     abg) step abg 600 python -u scripts/ab_gecko_variants.py ${AB_ARGS:-} > "$O/abg_${AB_NAME:-run}.txt" 2>&1 ;;
     *) echo "unknown step $s"; exit 2 ;;

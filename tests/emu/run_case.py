@@ -14,7 +14,8 @@ from hysteria_amd.salamander import SalamanderObfuscator  # noqa: E402
 from oracle import salamander_ref as ref  # noqa: E402
 
 
-def run(obf, psk, lens, in_off, inp, salts, out_cap, out_stride=0, pkt_cap=0, in_stride=0, len_uniform=0):
+def run(obf, psk, lens, in_off, inp, salts, out_cap, out_stride=0, pkt_cap=0, in_stride=0, len_uniform=0,
+        contiguous=False, expect_kernel=None):
     n = len(lens) if lens is not None else len(salts)
     co = ref.COracle()
     exp, eoff, elen, etot = co.batch(obf, psk, n, inp, in_off=in_off, in_stride=in_stride, in_len=lens,
@@ -26,9 +27,14 @@ def run(obf, psk, lens, in_off, inp, salts, out_cap, out_stride=0, pkt_cap=0, in
     total = np.zeros(1, np.uint64)
     o = SalamanderObfuscator(psk, 0)
     p = lambda a: None if a is None else a.ctypes.data  # noqa: E731
-    kw = dict(in_off=p(in_off), in_stride=in_stride, in_len=p(lens), len_uniform=len_uniform, out=p(out),
-              out_cap=out_cap, out_stride=out_stride, pkt_cap=pkt_cap, out_off=p(out_off), out_len=p(out_len),
-              out_total=p(total), stream=0)
+    kw = dict(in_off=None if contiguous else p(in_off), in_stride=in_stride, in_len=p(lens), len_uniform=len_uniform,
+              out=p(out), out_cap=out_cap, out_stride=out_stride, pkt_cap=pkt_cap, out_off=p(out_off),
+              out_len=p(out_len), out_total=p(total), stream=0)
+    if expect_kernel:
+        got_k = o.batch_kernel(obf, inp=p(inp), n=n, **{k: v for k, v in kw.items() if k != "stream"},
+                               **({"salts": p(salts)} if obf else {}))
+        want_k = os.environ.get("HYOBFS_KERNEL") == "wave" and "wave" or expect_kernel
+        assert got_k == want_k, ("kernel", got_k, want_k)
     if obf:
         o.obfuscate_batch(p(inp), n, salts=p(salts), **kw)
     else:
@@ -82,6 +88,53 @@ def case_packed_cap(seed, n, maxlen, obf, cap_pct, psk_len):
         inp, in_off, lens = wire, woff, wlen
     full = int(lens.sum()) + (8 * n if obf else 0)
     run(obf, psk, lens, in_off, inp, salts, max(16, full * cap_pct // 100))
+
+
+def case_contig(seed, n, dist, obf, cap_pct, psk_len, pkt_cap=0, misalign=0):
+    """Contiguous packed input (in_off NULL, in_stride 0: datagram i right after
+    datagram i-1) into packed output: the stream kernel (salamander_stream.h).  dist 0:
+    the bimodal 64/1350 mix; 1: 0..2100 B; 2: 0..40 B (many datagrams per tile, several
+    per chunk: multi-pass tiles); 3: 1000..5000 B; 4: bimodal with zero-length ones.
+    out_cap cut to cap_pct % of the full size, pkt_cap drops, deobfuscate of real wire
+    (8-byte wire datagrams dropped), misalign = input not 16-byte aligned (the fallback)."""
+    rng = np.random.default_rng(seed)
+    psk = bytes((11 * i + 5) & 0xFF for i in range(psk_len))
+    if dist == 0:
+        lens = ref.bimodal_lengths(3, seed, n)
+    elif dist == 1:
+        lens = rng.integers(0, 2100, n).astype(np.uint32)
+    elif dist == 2:
+        lens = rng.integers(0, 41, n).astype(np.uint32)
+    elif dist == 3:
+        lens = rng.integers(1000, 5000, n).astype(np.uint32)
+    else:
+        lens = ref.bimodal_lengths(3, seed, n)
+        lens[rng.random(n) < 0.05] = 0
+    lens = np.ascontiguousarray(lens, np.uint32)
+    in_off = np.zeros(n, np.uint64)
+    in_off[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+    total = int(lens.sum())
+    buf = np.zeros(total + 64 + 16, np.uint8)
+    base = (-buf.ctypes.data) % 16 + misalign
+    inp = buf[base:base + total + 32]
+    inp[:total] = rng.integers(0, 256, total, dtype=np.uint8)
+    salts = ref.splitmix64_array(2, seed, n)
+    if not obf:
+        co = ref.COracle()
+        cap = total + 8 * n
+        wire, woff, wlen, _ = co.batch(True, psk, n, inp, in_off=in_off, in_len=lens, salts=salts, out_cap=cap)
+        wl = int(wlen.sum())
+        wbuf = np.zeros(wl + 64 + 16, np.uint8)
+        wb = (-wbuf.ctypes.data) % 16 + misalign
+        winp = wbuf[wb:wb + wl + 32]
+        winp[:wl] = wire[:wl]
+        # the wire is contiguous: datagrams back to back, as their out_off say
+        assert np.array_equal(woff[1:], np.cumsum(wlen[:-1], dtype=np.uint64))
+        inp, in_off, lens, total = winp, woff, np.ascontiguousarray(wlen, np.uint32), wl
+    full = total + (8 * n if obf else 0)
+    want = "stream" if not misalign else "wave"
+    run(obf, psk, lens, in_off, inp, salts, max(16, full * cap_pct // 100), pkt_cap=pkt_cap, contiguous=True,
+        expect_kernel=want)
 
 
 def case_bimodal(n, obf):
@@ -312,6 +365,8 @@ if __name__ == "__main__":
     args = [int(a) for a in sys.argv[2:]]
     if which == "bimodal":
         case_bimodal(args[0], bool(args[1]))
+    elif which == "contig":
+        case_contig(*args)
     elif which == "pcap":
         case_packed_cap(*args[:3], bool(args[3]), args[4], args[5])
     elif which == "slotted":

@@ -46,6 +46,9 @@ SPECS = {
                                 "HYOBFS_KERNEL": "wave"}),
     "test_emulated_kernel_vs_oracle": lambda p: (p["which"], p["args"], {"HYEMU_CUS": p["cus"]}),
     "test_emulated_split_launches": lambda p: (p["which"], p["args"], dict(p["env"])),
+    "test_emulated_stream_kernel": lambda p: ("contig", p["args"], {"HYEMU_CUS": "2"}),
+    "test_emulated_contiguous_input_wave_forced": lambda p: ("contig", p["args"], {"HYEMU_CUS": "2",
+                                                                                   "HYOBFS_KERNEL": "wave"}),
 }
 
 
@@ -141,6 +144,30 @@ PACKED_CASES = [
     ("pcap", "7 500 1400 1 60 16"), ("pcap", "8 500 1400 0 70 127"), ("pcap", "9 17 3 1 100 4"),
     ("bimodal", "1000 1"), ("bimodal", "1000 0"),
 ]
+
+
+# Contiguous packed input (in_off NULL, in_stride 0) into packed output: the stream
+# kernel (salamander_stream.h) under AUTO, the prepass's input offsets + wave kernel when
+# forced (tests/emu/run_case.py case_contig: seed n dist obf cap% psk_len [pkt_cap misalign]).
+# Bimodal, 0..2100 B, tiny (multi-pass tiles, several datagrams per chunk), 1-5 KB,
+# zero-length datagrams; out_cap cuts, pkt_cap drops, real wire with 8-byte datagrams,
+# PSKs across salt words and the two-block case, a misaligned input (the fallback).
+CONTIG_CASES = [
+    "1 3000 0 1 100 16", "2 3000 0 0 100 16", "3 2000 1 1 100 16", "4 2000 1 0 100 33", "5 3000 2 1 100 16",
+    "6 3000 2 0 100 121", "7 300 3 1 100 16", "8 300 3 0 100 4", "9 3000 4 1 100 16", "10 3000 4 0 100 16",
+    "11 2000 1 1 60 16", "12 2000 1 0 70 127", "13 2000 1 1 100 16 1000", "14 2000 1 0 100 16 900",
+    "15 3000 0 1 100 16 0 1", "16 3000 0 0 100 16 0 1", "17 3000 2 1 50 16",
+]
+
+
+@pytest.mark.parametrize("args", CONTIG_CASES)
+def test_emulated_stream_kernel(emu_lib, args):
+    _run(emu_lib, "contig", args, {"HYEMU_CUS": "2"})
+
+
+@pytest.mark.parametrize("args", CONTIG_CASES[:6] + CONTIG_CASES[10:12])
+def test_emulated_contiguous_input_wave_forced(emu_lib, args):
+    _run(emu_lib, "contig", args, {"HYEMU_CUS": "2", "HYOBFS_KERNEL": "wave"})
 
 
 @pytest.mark.parametrize("which,args", PACKED_CASES)

@@ -367,6 +367,134 @@ def test_config3_bimodal_4M_digest(obfs, gpu, golden):
     assert h.hexdigest() == d["obf_sha256"]
 
 
+# ------------------------------------------- contiguous input: the stream kernel
+def _stream_expected(obfs):
+    return "wave" if getattr(obfs, "kernel", "auto") == "wave" else "stream"
+
+
+def test_contiguous_bimodal_64k_vs_oracle_and_digest(obfs, gpu, coracle, golden):
+    """Contiguous packed input (in_off NULL, in_stride 0: datagram i right after
+    datagram i-1, include/hyobfs.h) into packed output: the stream kernel
+    (salamander_stream.h) under auto, the prepass's offsets + wave kernel under wave.
+    The wire equals the explicit-offset batch's (the committed digest and the C
+    oracle byte for byte); the wire, itself contiguous, deobfuscates back."""
+    import torch
+    d = golden[1]["bimodal_64k"]
+    n = d["n"]
+    lens, in_off, inp, salts, total_in = _bimodal(gpu, n)
+    cap = total_in + 8 * n
+    out = torch.full((cap + 64,), 0xA5, dtype=torch.uint8, device=gpu)
+    out_off = torch.empty(n, dtype=torch.int64, device=gpu)
+    out_len = torch.empty(n, dtype=torch.int32, device=gpu)
+    total = torch.zeros(1, dtype=torch.int64, device=gpu)
+    kw = dict(in_len=lens, out=out, out_cap=cap, out_off=out_off, out_len=out_len, out_total=total)
+    assert obfs.batch_kernel(True, inp=inp, n=n, salts=salts, **kw) == _stream_expected(obfs)
+    obfs.obfuscate_batch(inp, n, salts=salts, **kw)
+    got = _host(out)
+    assert hashlib.sha256(got[:cap].tobytes()).hexdigest() == d["obf_sha256"]
+    assert (got[cap:] == 0xA5).all()
+    h_lens = _host(lens).view(np.uint32)
+    exp, eoff, elen, etot = coracle.batch(True, PSK, n, _host(inp), in_off=_host(in_off).view(np.uint64),
+                                          in_len=h_lens, salts=coracle.salts(2, 0, n), out_cap=cap)
+    assert np.array_equal(got[:cap], exp)
+    assert np.array_equal(_host(out_off).view(np.uint64), eoff)
+    assert np.array_equal(_host(out_len).view(np.uint32), elen)
+    assert int(_host(total)[0]) == etot
+    back = torch.full((total_in + 64,), 0x5A, dtype=torch.uint8, device=gpu)
+    kw = dict(in_len=out_len, out=back, out_cap=total_in, out_total=total)
+    assert obfs.batch_kernel(False, inp=out, n=n, **kw) == _stream_expected(obfs)
+    obfs.deobfuscate_batch(out, n, **kw)
+    hb = _host(back)
+    assert np.array_equal(hb[:total_in], _host(inp)[:total_in])
+    assert (hb[total_in:] == 0x5A).all() and int(_host(total)[0]) == total_in
+
+
+def test_contiguous_config3_4M_digest_and_roundtrip(obfs, gpu, golden):
+    """BASELINE configs[2] at full size through the contiguous layout (what bench.py runs):
+    the committed 4M digest, and the device round trip."""
+    import torch
+    d = golden[1]["config3_bimodal_4M"]
+    n = d["n"]
+    lens, in_off, inp, salts, total_in = _bimodal(gpu, n)
+    del in_off
+    cap = total_in + 8 * n
+    out = torch.empty(cap, dtype=torch.uint8, device=gpu)
+    out_len = torch.empty(n, dtype=torch.int32, device=gpu)
+    obfs.obfuscate_batch(inp, n, in_len=lens, salts=salts, out=out, out_cap=cap, out_len=out_len)
+    h = hashlib.sha256()
+    torch.cuda.synchronize()
+    step = 1 << 28
+    for s in range(0, cap, step):
+        h.update(out[s:s + step].cpu().numpy().tobytes())
+    assert h.hexdigest() == d["obf_sha256"]
+    back = torch.empty(total_in + 16, dtype=torch.uint8, device=gpu)
+    obfs.deobfuscate_batch(out, n, in_len=out_len, out=back, out_cap=total_in)
+    torch.cuda.synchronize()
+    assert torch.equal(back[:total_in], inp[:total_in])
+
+
+# seed, n, length distribution, obfuscate, out_cap %, PSK length, pkt_cap, input misalignment
+# (dist 0 bimodal, 1: 0..2100 B, 2: 0..40 B (multi-pass tiles), 3: 1..5 KB, 4: bimodal + zeros)
+CONTIG_GPU = [(1, 20000, 0, 1, 100, 16, 0, 0), (2, 20000, 0, 0, 100, 16, 0, 0), (3, 8000, 1, 1, 100, 33, 0, 0),
+              (4, 8000, 1, 0, 100, 121, 0, 0), (5, 20000, 2, 1, 100, 16, 0, 0), (6, 20000, 2, 0, 100, 4, 0, 0),
+              (7, 2000, 3, 1, 100, 127, 0, 0), (8, 2000, 3, 0, 100, 16, 0, 0), (9, 20000, 4, 1, 100, 16, 0, 0),
+              (10, 20000, 4, 0, 100, 16, 0, 0), (11, 8000, 1, 1, 60, 16, 0, 0), (12, 8000, 1, 0, 70, 16, 0, 0),
+              (13, 8000, 1, 1, 100, 16, 1000, 0), (14, 8000, 1, 0, 100, 16, 900, 0), (15, 20000, 0, 1, 100, 16, 0, 1),
+              (16, 20000, 0, 0, 100, 16, 0, 3)]
+
+
+@pytest.mark.parametrize("case", CONTIG_GPU)
+def test_contiguous_input_grid_vs_oracle(obfs, gpu, coracle, case):
+    """The stream kernel's edge cases byte for byte against the C oracle, sentinel bytes
+    past the output: tiles with more than 64 datagrams and several per 16-byte chunk,
+    zero-length datagrams, out_cap cuts (the tail), pkt_cap drops (holes in the input),
+    real wire with 8-byte datagrams, PSKs across salt words and two blocks, misaligned
+    input (the offsets + wave kernel fallback)."""
+    import torch
+    seed, n, dist, obf, cap_pct, psk_len, pkt_cap, mis = case
+    rng = np.random.default_rng(seed)
+    psk = bytes((11 * i + 5) & 0xFF for i in range(psk_len))
+    lens = {0: lambda: ref.bimodal_lengths(3, seed, n), 1: lambda: rng.integers(0, 2100, n),
+            2: lambda: rng.integers(0, 41, n), 3: lambda: rng.integers(1000, 5000, n),
+            4: lambda: np.where(rng.random(n) < 0.05, 0, ref.bimodal_lengths(3, seed, n))}[dist]()
+    lens = np.ascontiguousarray(lens, np.uint32)
+    in_off = np.concatenate([[0], np.cumsum(lens[:-1], dtype=np.uint64)]).astype(np.uint64)
+    total = int(lens.sum())
+    inp = rng.integers(0, 256, total + 32, dtype=np.uint8)
+    salts = ref.splitmix64_array(2, seed, n)
+    if not obf:
+        wire, woff, wlen, _ = coracle.batch(True, psk, n, inp, in_off=in_off, in_len=lens, salts=salts,
+                                            out_cap=total + 8 * n)
+        inp, in_off, lens, total = np.concatenate([wire, np.zeros(32, np.uint8)]), woff, wlen.copy(), int(wlen.sum())
+    full = total + (8 * n if obf else 0)
+    cap = max(16, full * cap_pct // 100)
+    exp, eoff, elen, etot = coracle.batch(bool(obf), psk, n, inp, in_off=in_off, in_len=lens,
+                                          salts=salts if obf else None, out_cap=cap, pkt_cap=pkt_cap)
+    d_in = torch.zeros(len(inp) + 16, dtype=torch.uint8, device=gpu)
+    d_in[mis:mis + len(inp)] = torch.from_numpy(inp).to(gpu)
+    src = d_in[mis:]
+    out = torch.full((cap + 64,), 0xA5, dtype=torch.uint8, device=gpu)
+    out_off = torch.zeros(n, dtype=torch.int64, device=gpu)
+    out_len = torch.zeros(n, dtype=torch.int32, device=gpu)
+    tot = torch.zeros(1, dtype=torch.int64, device=gpu)
+    kw = dict(in_len=_u32(lens, gpu), out=out, out_cap=cap, pkt_cap=pkt_cap, out_off=out_off, out_len=out_len,
+              out_total=tot)
+    if obf:
+        kw["salts"] = _u64(salts, gpu)
+    want = "wave" if mis or getattr(obfs, "kernel", "auto") == "wave" else "stream"
+    assert obfs.batch_kernel(bool(obf), inp=src, n=n, **kw) == want
+    (obfs.obfuscate_batch if obf else obfs.deobfuscate_batch)(inp=src, n=n, **kw)
+    got = _host(out)
+    assert np.array_equal(_host(out_off).view(np.uint64), eoff)
+    assert np.array_equal(_host(out_len).view(np.uint32), elen)
+    assert int(_host(tot)[0]) == etot
+    written = np.zeros(cap + 64, bool)
+    for o, w in zip(eoff, elen):
+        written[int(o):int(o) + int(w)] = True
+    assert np.array_equal(got[written], exp[written[:cap]])
+    assert (got[~written] == 0xA5).all()
+
+
 def _ragged_case(seed, n, maxlen, gap_max, base_misalign):
     rng = np.random.default_rng(seed)
     lens = rng.integers(0, maxlen, n).astype(np.uint32)
