@@ -45,7 +45,7 @@ constexpr uint32_t kSIn = kST + 1024;          // staged input bytes (deobfuscat
 constexpr uint32_t kSGuard = 16;               // LDS bytes before the stage (funnel reads at pos >= -16)
 constexpr int kSBlk = 1024;                    // datagrams per prepass block (256 threads x 4)
 #ifndef HY_STREAM_U
-#define HY_STREAM_U 4
+#define HY_STREAM_U 2
 #endif
 constexpr int kSU = HY_STREAM_U;               // sweep chunks per thread in flight
 
@@ -302,8 +302,11 @@ __device__ __forceinline__ int32_t stream_cand(int32_t o, uint32_t W, int32_t sa
     return t == 0 ? (o >> 4) : t == 1 ? ((o + salt) >> 4) : ((o + (int32_t)W - 1) >> 4);
 }
 
+#ifndef HY_STREAM_WAVES
+#define HY_STREAM_WAVES 5   // min waves per SIMD (6 spills at 80 VGPRs; the LDS allows 6 workgroups of 24 KB per CU)
+#endif
 template <bool OBF, int SW>
-__global__ __launch_bounds__(256) void salamander_stream_kernel(BatchParams B, KeyParams K, StreamParams SP) {
+__global__ __launch_bounds__(256, HY_STREAM_WAVES) void salamander_stream_kernel(BatchParams B, KeyParams K, StreamParams SP) {
     constexpr int32_t SALT = OBF ? 8 : 0;   // salt bytes in front of the output payload
     constexpr int64_t SKIP = OBF ? 0 : 8;   // salt bytes in front of the input payload
     __shared__ __attribute__((aligned(16))) StreamLDS S;
@@ -490,7 +493,10 @@ __global__ __launch_bounds__(256) void salamander_stream_kernel(BatchParams B, K
                     if (ok[u]) store16_stream(ob + x, v[u]);
                 }
             }
-            __syncthreads();   // LDS reuse: the next pass / tile overwrites metadata and stage
+            // LDS reuse: the next pass / tile overwrites metadata and stage.  Only the LDS
+            // reads must be done (no vmcnt wait): the next tile's DMA goes out while this
+            // tile's stores are still in flight
+            hy_lds_barrier();
         }
     }
 }
