@@ -683,6 +683,10 @@ int hyobfs_shard_bounds(const uint32_t* in_len, uint64_t n, int nshards, uint64_
 // the encode kernel derives keys in registers: no workspace
 uint64_t hyobfs_gecko_workspace_size(uint64_t) { return 0; }
 
+uint64_t hyobfs_gecko_workspace_bytes(const hyobfs_gecko_batch* b) {
+    return b ? hyobfs::gecko_tiles_workspace_bytes(b->out_cap) : 0;
+}
+
 int hyobfs_gecko_encode_batch(hyobfs_salamander* c, const hyobfs_gecko_batch* b, void* stream) {
     if (!c || !b) return HYOBFS_ERR_INVALID;
     if (b->n == 0) return HYOBFS_OK;
@@ -694,12 +698,22 @@ int hyobfs_gecko_encode_batch(hyobfs_salamander* c, const hyobfs_gecko_batch* b,
     bool zero_key = true;
     for (int i = 0; i < 32; ++i) zero_key = zero_key && b->pad_key[i] == 0;
     if (zero_key) return HYOBFS_ERR_INVALID;
-    const uint64_t ws_need = hyobfs_gecko_workspace_size(b->n);
-    if (ws_need && (!b->workspace || b->workspace_bytes < ws_need)) return HYOBFS_ERR_INVALID;
+    const uint64_t ws_need = hyobfs_gecko_workspace_bytes(b);
+    if (ws_need && b->workspace && b->workspace_bytes < ws_need) return HYOBFS_ERR_INVALID;
     DeviceGuard g(c->device);
     if (!g.ok) return HYOBFS_ERR_HIP;
-    return hyobfs::launch_gecko_encode(c->kp, *b, static_cast<hipStream_t>(stream)) == hipSuccess ? HYOBFS_OK
-                                                                                                : HYOBFS_ERR_HIP;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    void* ws = ws_need ? b->workspace : nullptr;
+    void* scratch = nullptr;
+    if (ws_need && !ws) {   // the context's pool, freed behind the launch in stream order
+        hipMemPool_t pool = scratch_pool(c);
+        if (!pool) return HYOBFS_ERR_HIP;
+        if (hipMallocFromPoolAsync(&scratch, ws_need, pool, s) != hipSuccess) return HYOBFS_ERR_NOMEM;
+        ws = scratch;
+    }
+    const hipError_t e = hyobfs::launch_gecko_encode(c->kp, *b, ws, s);
+    if (scratch && hipFreeAsync(scratch, s) != hipSuccess) return HYOBFS_ERR_HIP;
+    return e == hipSuccess ? HYOBFS_OK : HYOBFS_ERR_HIP;
 }
 
 int hyobfs_gecko_parse_batch(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint64_t n,

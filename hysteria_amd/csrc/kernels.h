@@ -84,7 +84,9 @@ uint64_t batch_workspace_bytes(bool obfuscate, const BatchParams& b);
 inline bool contiguous_input(const BatchParams& b) { return !b.in_off && b.in_stride == 0 && b.in_len && b.n > 1; }
 hipError_t launch_keys(const KeyParams& k, const uint64_t* salts, uint8_t* keys, uint64_t n,
                        hipStream_t s);
-hipError_t launch_gecko_encode(const KeyParams& k, const hyobfs_gecko_batch& b, hipStream_t s);
+// ws: gecko_tiles_workspace_bytes(b.out_cap) bytes (NULL or out_cap 0: the wave-group kernel only)
+hipError_t launch_gecko_encode(const KeyParams& k, const hyobfs_gecko_batch& b, void* ws, hipStream_t s);
+uint64_t gecko_tiles_workspace_bytes(uint64_t out_cap);
 hipError_t launch_gecko_parse(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint64_t n,
                               hyobfs_gecko_parsed* out, hipStream_t s);
 hipError_t launch_synth_stream(uint8_t* dst, uint64_t nbytes, uint64_t seed, uint64_t start,

@@ -8,7 +8,8 @@ between processes).
       python scripts/ab_gecko_variants.py
 
 A name ending in "!" is an ablation build (wrong output): its wire is not checked
-against the first build's."""
+against the first build's.  AB_GK_MODES (default "tile,wave") runs each build through
+the wire-tile kernel (out_cap given) and the wave-group kernel (no out_cap)."""
 import os
 import statistics
 import sys
@@ -36,18 +37,23 @@ out = torch.empty(total + 16, dtype=torch.uint8, device=dev)
 dfr = torch.from_numpy(fr.view(np.uint8)).to(dev)
 doff = torch.from_numpy(off.view(np.uint8)).to(dev)
 alg = M * L + total
+modes = os.environ.get("AB_GK_MODES", "tile,wave").split(",")
+ws = torch.empty(max(16, gecko.workspace_bytes(out.numel())), dtype=torch.uint8, device=dev)
 obs = {name: hysteria_amd.SalamanderObfuscator(b"average_password", 0, lib_path=path) for name, path in libs}
+libs = [(f"{name}/{m}", path) for name, path in libs for m in modes]
+obs = {f"{name}/{m}": o for name, o in obs.items() for m in modes}
 
 
-def run(o):
-    gecko.encode_batch(o, msg=msg, frames=dfr, salts=salts, pad_key=bytes(range(32)), pad_nonce=bytes(12), out=out,
-                       out_off=doff, n=nf)
+def run(name):
+    cap = out.numel() if name.endswith("/tile") else 0
+    gecko.encode_batch(obs[name], msg=msg, frames=dfr, salts=salts, pad_key=bytes(range(32)), pad_nonce=bytes(12),
+                       out=out, out_off=doff, n=nf, out_cap=cap, workspace=ws, workspace_bytes=ws.numel())
 
 
 ref = None
 for name, _ in libs:
     out.fill_(0)
-    run(obs[name])
+    run(name)
     torch.cuda.synchronize()
     if ref is None:
         ref = out.clone()
@@ -57,11 +63,11 @@ times = {name: [] for name, _ in libs}
 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 for _ in range(R):
     for name, _ in libs:
-        run(obs[name])
+        run(name)
         torch.cuda.synchronize()
         e0.record()
         for _ in range(K):
-            run(obs[name])
+            run(name)
         e1.record()
         torch.cuda.synchronize()
         times[name].append(e0.elapsed_time(e1) / K)
@@ -70,5 +76,5 @@ for name, _ in libs:
     ms = statistics.median(times[name])
     print(f"{name:14s} {ms:.4f} ms  {alg / ms / 1e6:7.1f} GB/s ({alg / ms / 1e6 / 8000 * 100:5.1f} % of 8 TB/s)  "
           f"min {min(times[name]):.4f}")
-for o in obs.values():
+for o in set(obs.values()):
     o.close()

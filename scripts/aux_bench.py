@@ -48,7 +48,7 @@ hysteria_amd.synth_stream(msg, M * L, 1, 0)
 salts = torch.empty(nf, dtype=torch.int64, device=dev)
 hysteria_amd.synth_u64(salts, nf, 2, 0)
 out = torch.empty(total + 16, dtype=torch.uint8, device=dev)
-ws = torch.empty(gecko.workspace_size(nf), dtype=torch.uint8, device=dev)
+ws = torch.empty(max(16, gecko.workspace_bytes(out.numel())), dtype=torch.uint8, device=dev)   # wire tiles
 o = hysteria_amd.SalamanderObfuscator(b"average_password", 0)
 dfr, doff = d(fr), d(off)
 ms = timed(lambda: gecko.encode_batch(o, msg=msg, frames=dfr, salts=salts, pad_key=bytes(range(1, 33)), pad_nonce=bytes(12), out=out, out_off=doff,

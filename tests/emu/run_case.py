@@ -234,7 +234,7 @@ def case_host(n, L, chunk, obf):
         assert out[i * out_stride:i * out_stride + len(exp)].tobytes() == exp, i
 
 
-def case_gecko(n_msgs, seed, layout=0):
+def case_gecko(n_msgs, seed, layout=0, tiles=1):
     """Gecko frames: one device encode pass vs oracle/gecko_ref, then deobfuscate + parse.
     layout 0: packed wire order (the aligned sweep); 1: ascending with gaps between
     frames (aligned sweep, gap bytes untouched); 2: frames placed in shuffled order
@@ -271,12 +271,18 @@ def case_gecko(n_msgs, seed, layout=0):
         off, total = pos, int(cur)
     salts = ref.splitmix64_array(5, 0, nf)
     out = np.full(total + 64, 0xA5, np.uint8)
-    ws = np.zeros(gecko.workspace_size(nf), np.uint8)
     o = SalamanderObfuscator(psk, 0)
     p = lambda a: a.ctypes.data  # noqa: E731
     key, nonce = bytes(range(3, 35)), bytes(range(40, 52))
+    # out_cap given: frames in order run the wire-tile kernel (layouts 0, 1, 3), shuffled
+    # ones (layout 2) the wave-group kernel; tiles=0 runs the wave-group kernel only
+    out_cap = total + 64 if tiles else 0
+    ws = np.full(max(gecko.workspace_bytes(out_cap), 16), 0xEE, np.uint8)
     gecko.encode_batch(o, msg=p(msg), frames=p(fr), salts=p(salts), pad_key=key, pad_nonce=nonce, out=p(out),
-                       out_off=p(off), workspace=p(ws), n=nf, stream=0)
+                       out_off=p(off), n=nf, stream=0, out_cap=out_cap, workspace=p(ws),
+                       workspace_bytes=gecko.workspace_bytes(out_cap))
+    if tiles:   # which kernel ran: the scratch's word at +8 is 0 when the wire tiles took the batch
+        assert int(ws[8:12].view(np.uint32)[0]) == (1 if layout == 2 else 0), ("tiled", layout)
     exp = gref.encode_wire(psk, msg.tobytes(), fr.tolist(), salts, key, nonce, off)
     assert out[total:].tobytes() == b"\xa5" * 64
     written = np.zeros(total + 64, bool)

@@ -115,6 +115,9 @@ CASES = [
     ("gecko", "60 8 1", "2"),            # ... ascending frames with gaps: gap bytes untouched
     ("gecko", "60 9 2", "2"),            # ... shuffled placement: the per-frame path
     ("gecko", "70 10 3", "2"),           # ... tiny frames, several per 16-byte chunk
+    ("gecko", "300 11 0", "2"),          # ... the wire-tile kernel over several tiles
+    ("gecko", "40 7 0 0", "2"),          # ... no out_cap: the wave-group kernel alone
+    ("gecko", "60 8 1 0", "2"),
     ("punch", "300 5 3", "2"),           # realm punch matcher (realm.hip)
     ("quic", "2", "2"),                  # QUIC Initial unprotect + ReadCryptoPayload kernels (quic.hip)
 ]

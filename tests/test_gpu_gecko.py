@@ -29,8 +29,13 @@ def _messages(n, seed):
     return lens, msg
 
 
-@pytest.mark.parametrize("n_msgs,lo,hi", [(1, 512, 1200), (300, 512, 1200), (500, 400, 900), (64, 2048, 2048)])
-def test_encode_batch_vs_oracle(gpu, n_msgs, lo, hi):
+@pytest.mark.parametrize("tiles", [True, False])
+@pytest.mark.parametrize("n_msgs,lo,hi", [(1, 512, 1200), (300, 512, 1200), (500, 400, 900), (64, 2048, 2048),
+                                          (3000, 512, 1200)])
+def test_encode_batch_vs_oracle(gpu, n_msgs, lo, hi, tiles):
+    """Device frames byte for byte against oracle/gecko_ref.py: through the wire-tile
+    kernel (out_cap given, frames in wire order; asserted through the workspace's flag)
+    and through the wave-group kernel (no out_cap)."""
     import torch
     import hysteria_amd
     from hysteria_amd import gecko
@@ -41,10 +46,14 @@ def test_encode_batch_vs_oracle(gpu, n_msgs, lo, hi):
     o = hysteria_amd.SalamanderObfuscator(PSK, 0)
     try:
         out = torch.full((total + 64,), 0xA5, dtype=torch.uint8, device=gpu)
-        ws = torch.empty(gecko.workspace_size(nf), dtype=torch.uint8, device=gpu)
+        cap = total + 64 if tiles else 0
+        ws = torch.full((max(16, gecko.workspace_bytes(cap)),), 0xEE, dtype=torch.uint8, device=gpu)
         gecko.encode_batch(o, msg=_dev(msg, gpu), frames=_dev(fr, gpu), salts=_dev(salts, gpu), pad_key=KEY, pad_nonce=NONCE,
-                           out=out, out_off=_dev(off, gpu), workspace=ws, n=nf)
+                           out=out, out_off=_dev(off, gpu), workspace=ws, n=nf, out_cap=cap,
+                           workspace_bytes=gecko.workspace_bytes(cap))
         got = out.cpu().numpy()
+        if tiles:
+            assert int(ws[8:12].cpu().numpy().view(np.uint32)[0]) == 0, "the wire-tile kernel did not run"
     finally:
         o.close()
     exp = gref.encode_wire(PSK, msg.tobytes(), fr.tolist(), salts, KEY, NONCE, off)
