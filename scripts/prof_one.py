@@ -1,7 +1,8 @@
 """Minimal driver for rocprofv3 counter passes: K obfuscate + K deobfuscate launches
 of the uniform 1M x 1200 B batch (BASELINE configs[1]), or of the 4M bimodal
-batch (configs[2], packed output) with 'bimodal'.  Optional 3rd argument: the
-context's kernel (auto|wave|persistent|uniform)."""
+batch (configs[2], packed output) with 'bimodal' (contiguous input, as bench.py) or
+'bimodal_off' (explicit offsets).  Optional 3rd argument: the context's kernel
+(auto|wave|persistent|uniform)."""
 import os, sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch, hysteria_amd
@@ -23,7 +24,9 @@ if wl == "uniform":
 else:
     P = 1 << 22
     lens = torch.empty(P, dtype=torch.int32, device=dev); hysteria_amd.synth_bimodal_lengths(lens, P, 3, 0)
-    in_off = torch.zeros(P, dtype=torch.int64, device=dev); in_off[1:] = torch.cumsum(lens[:-1].to(torch.int64), 0)
+    in_off = None
+    if wl == "bimodal_off":
+        in_off = torch.zeros(P, dtype=torch.int64, device=dev); in_off[1:] = torch.cumsum(lens[:-1].to(torch.int64), 0)
     total_in = int(lens.to(torch.int64).sum())
     inp = torch.empty(total_in + 16, dtype=torch.uint8, device=dev); hysteria_amd.synth_stream(inp, total_in, 1, 0)
     salts = torch.empty(P, dtype=torch.int64, device=dev); hysteria_amd.synth_u64(salts, P, 2, 0)
@@ -32,12 +35,14 @@ else:
     out_off = torch.empty(P, dtype=torch.int64, device=dev)
     out_len = torch.empty(P, dtype=torch.int32, device=dev)
     back = torch.empty(total_in + 16, dtype=torch.uint8, device=dev)
-    ws = torch.empty(hysteria_amd.workspace_size(P), dtype=torch.uint8, device=dev)
+    nws = max(o.workspace_bytes(inp=inp, n=P, in_off=in_off, in_len=lens, out=wire, out_cap=cap),
+              o.workspace_bytes(inp=wire, n=P, in_off=None if in_off is None else out_off, in_len=out_len, out=back, out_cap=total_in))
+    ws = torch.empty(max(nws, 16), dtype=torch.uint8, device=dev)
     for _ in range(K):
         o.obfuscate_batch(inp, P, in_off=in_off, in_len=lens, salts=salts, out=wire, out_cap=cap,
                           out_off=out_off, out_len=out_len, workspace=ws, workspace_bytes=ws.numel())
     for _ in range(K):
-        o.deobfuscate_batch(wire, P, in_off=out_off, in_len=out_len, out=back, out_cap=total_in,
+        o.deobfuscate_batch(wire, P, in_off=None if in_off is None else out_off, in_len=out_len, out=back, out_cap=total_in,
                             workspace=ws, workspace_bytes=ws.numel())
 torch.cuda.synchronize()
 print("done", wl, K, kern)
