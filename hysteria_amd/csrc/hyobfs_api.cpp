@@ -534,7 +534,7 @@ void hyobfs_salamander_free(hyobfs_salamander* c) { hyobfs::ctx_release(c); }
 int hyobfs_salamander_device(const hyobfs_salamander* c) { return c ? c->device : -1; }
 
 int hyobfs_salamander_set_kernel(hyobfs_salamander* c, int kernel) {
-    if (!c || kernel < HYOBFS_KERNEL_AUTO || kernel > HYOBFS_KERNEL_TILE) return HYOBFS_ERR_INVALID;
+    if (!c || kernel < HYOBFS_KERNEL_AUTO || kernel > HYOBFS_KERNEL_STREAM) return HYOBFS_ERR_INVALID;
     c->kernel = kernel;
     return HYOBFS_OK;
 }
@@ -622,13 +622,14 @@ uint64_t hyobfs_batch_workspace_bytes(const hyobfs_batch* b) {
     bp.in_len = b->in_len;
     bp.out_cap = b->out_cap;
     bp.out_stride = b->out_stride;
-    // the larger of the stream kernel's and the fallback's needs: independent of the
-    // context's kernel choice
-    bp.kernel = hyobfs::kKernelAuto;
-    const uint64_t a = hyobfs::batch_workspace_bytes(true, bp);
-    bp.kernel = hyobfs::kKernelWave;
-    const uint64_t w = hyobfs::batch_workspace_bytes(true, bp);
-    return a > w ? a : w;
+    // the largest need over the kernel choices: independent of the context's
+    uint64_t m = 0;
+    for (int k : {hyobfs::kKernelAuto, hyobfs::kKernelWave, hyobfs::kKernelStream}) {
+        bp.kernel = k;
+        const uint64_t v = hyobfs::batch_workspace_bytes(true, bp);
+        m = v > m ? v : m;
+    }
+    return m;
 }
 
 uint64_t hyobfs_batch_workspace_size(uint64_t n) {

@@ -64,6 +64,10 @@ struct BatchParams {
     unsigned long long* out_total;
     const uint64_t* tile_prefix;  // packed: exclusive prefix of tile sums (ntiles+1)
     uint64_t* tile_sums;          // packed: scratch, ntiles+1 entries
+    // contiguous input, packed output on the wave kernel: per-tile sums of the input
+    // lengths (scratch, ntiles+1) and their exclusive prefix (the input offsets)
+    uint64_t* in_tile_sums = nullptr;
+    const uint64_t* in_tile_prefix = nullptr;
     void* scratch;                // contiguous input: the stream prepass's scratch (batch_workspace_bytes)
     uint32_t run_log2;            // wave kernel: datagrams per run = 2^run_log2
     uint64_t blk0 = 0;            // wave kernel, packed runs of 64: first workgroup of this launch

@@ -38,63 +38,87 @@ HY_EXTERN_SW(12) HY_EXTERN_SW(13) HY_EXTERN_SW(14) HY_EXTERN_SW(15)
 
 // ------------------------------------------------------ packed-layout scan
 // Tile sums of the output widths; the main kernel adds a wavefront scan.
+// Per tile of kTile datagrams: the sum of the output widths (packed layout) and, for
+// contiguous input, of the input lengths.  Wave w of workgroup b owns tile 4b + w,
+// four datagrams per lane; no LDS, no barrier.
 template <bool OBF>
-__global__ __launch_bounds__(kTile) void tile_sums_kernel(BatchParams B) {
-    __shared__ uint64_t s_w[kTile / 64];
-    const uint64_t p = (uint64_t)blockIdx.x * kTile + threadIdx.x;
-    uint32_t W = 0;
-    if (p < B.n) W = out_width<OBF>(pkt_len(B, p), B.pkt_cap);
-    const uint64_t ws = wave_sum(W);
-    if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = ws;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        uint64_t s = 0;
+__global__ __launch_bounds__(256) void tile_sums_kernel(BatchParams B, uint64_t ntiles) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t tile = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const uint64_t p0 = tile * kTile + 4ull * lane;
+    uint64_t sw = 0, sl = 0;
 #pragma unroll
-        for (int i = 0; i < kTile / 64; ++i) s += s_w[i];
-        B.tile_sums[blockIdx.x] = s;
+    for (int k = 0; k < 4; ++k) {
+        if (p0 + k < B.n) {
+            const uint32_t L = pkt_len(B, p0 + k);
+            sw += out_width<OBF>(L, B.pkt_cap);
+            sl += L;
+        }
+    }
+    sw = wave_sum(sw);
+    if (B.in_tile_sums) sl = wave_sum(sl);
+    if (lane == 0 && tile < ntiles) {
+        B.tile_sums[tile] = sw;
+        if (B.in_tile_sums) B.in_tile_sums[tile] = sl;
     }
 }
 
-// Exclusive scan of ntiles values in place, one workgroup of 1024 threads,
-// each owning 16 consecutive values per pass (one pass covers 16384 tiles = 4M
-// datagrams); writes the total at [ntiles].  (A stride-1024 loop with three
+// Exclusive scan of ntiles values in place -- of v, and of v2 in the same pass when
+// given (contiguous input: the length sums) -- one workgroup of 1024 threads, each
+// owning 16 consecutive values per pass (one pass covers 16384 tiles = 4M
+// datagrams); writes the totals at [ntiles].  (A stride-1024 loop with three
 // barriers per 1024 values took 25 us for 16384 tiles.)
-__global__ __launch_bounds__(1024) void scan_tiles_kernel(uint64_t* v, uint64_t ntiles) {
-    constexpr int PER = 16;
-    __shared__ uint64_t s_w[16];
-    __shared__ uint64_t s_carry;
+template <bool TWO>
+__global__ __launch_bounds__(1024) void scan_tiles_kernel(uint64_t* v, uint64_t* v2, uint64_t ntiles) {
+    constexpr int PER = 16, NA = TWO ? 2 : 1;
+    __shared__ uint64_t s_w[NA][16];
+    __shared__ uint64_t s_carry[NA];
     const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
-    if (t == 0) s_carry = 0;
+    if (t < NA) s_carry[t] = 0;
     __syncthreads();
     for (uint64_t base = 0; base < ntiles; base += 1024 * PER) {
         const uint64_t i0 = base + (uint64_t)t * PER;
-        uint64_t x[PER], sum = 0;
+        uint64_t x[NA][PER], sum[NA], inc[NA];
 #pragma unroll
-        for (int k = 0; k < PER; ++k) {
-            x[k] = i0 + k < ntiles ? v[i0 + k] : 0;
-            sum += x[k];
-        }
-        const uint64_t inc = wave_incl_scan(sum, lane);
-        if (lane == 63) s_w[wid] = inc;
-        __syncthreads();
-        uint64_t wpre = 0, tot = 0;
-        for (int w = 0; w < 16; ++w) {
-            const uint64_t sw = s_w[w];
-            wpre += (w < wid) ? sw : 0;
-            tot += sw;
-        }
-        const uint64_t carry = s_carry;
-        uint64_t run = carry + wpre + inc - sum;
+        for (int a = 0; a < NA; ++a) {
+            uint64_t* const arr = a ? v2 : v;
+            sum[a] = 0;
 #pragma unroll
-        for (int k = 0; k < PER; ++k) {
-            if (i0 + k < ntiles) v[i0 + k] = run;
-            run += x[k];
+            for (int k = 0; k < PER; ++k) {
+                x[a][k] = i0 + k < ntiles ? arr[i0 + k] : 0;
+                sum[a] += x[a][k];
+            }
+        }
+#pragma unroll
+        for (int a = 0; a < NA; ++a) {
+            inc[a] = wave_incl_scan(sum[a], lane);
+            if (lane == 63) s_w[a][wid] = inc[a];
         }
         __syncthreads();
-        if (t == 0) s_carry = carry + tot;
+#pragma unroll
+        for (int a = 0; a < NA; ++a) {
+            uint64_t* const arr = a ? v2 : v;
+            uint64_t wpre = 0;
+            for (int w = 0; w < wid; ++w) wpre += s_w[a][w];
+            uint64_t run = s_carry[a] + wpre + inc[a] - sum[a];
+#pragma unroll
+            for (int k = 0; k < PER; ++k) {
+                if (i0 + k < ntiles) arr[i0 + k] = run;
+                run += x[a][k];
+            }
+        }
+        __syncthreads();
+        if (t < NA) {
+            uint64_t tot = 0;
+            for (int w = 0; w < 16; ++w) tot += s_w[t][w];
+            s_carry[t] += tot;
+        }
         __syncthreads();
     }
-    if (t == 0) v[ntiles] = s_carry;
+    if (t == 0) {
+        v[ntiles] = s_carry[0];
+        if (TWO) v2[ntiles] = s_carry[NA - 1];
+    }
 }
 
 // keys only (hyobfs_salamander_key): key[i] = BLAKE2b-256(PSK || salts[i])
@@ -152,12 +176,17 @@ __global__ void synth_bimodal_kernel(uint32_t* dst, uint64_t n, uint64_t seed, u
 // Kernel choice ("Kernels"): AUTO runs the tile kernel where it
 // applies (tile_params) and the wave kernel elsewhere; WAVE forces the wave
 // kernel; TILE asks for the tile kernel (falls back to the wave kernel where it
-// does not apply).  HYOBFS_KERNEL=wave|tile sets what AUTO means in a process.
+// does not apply); STREAM asks for the stream kernel on contiguous packed input
+// (the wave kernel elsewhere).  HYOBFS_KERNEL=wave|tile|stream sets what AUTO
+// means in a process.
 static int kernel_override() {   // HYOBFS_KERNEL, as HYOBFS_KERNEL_* (0 = auto); read once, thread-safe
     static const int v = [] {
         const char* e = std::getenv("HYOBFS_KERNEL");
-        return !e ? kKernelAuto : std::strcmp(e, "wave") == 0 ? kKernelWave : std::strcmp(e, "tile") == 0 ? kKernelTile
-                                                                                                        : kKernelAuto;
+        return !e                          ? kKernelAuto
+               : std::strcmp(e, "wave") == 0   ? kKernelWave
+               : std::strcmp(e, "tile") == 0   ? kKernelTile
+               : std::strcmp(e, "stream") == 0 ? kKernelStream
+                                               : kKernelAuto;
     }();
     return v;
 }
@@ -189,13 +218,20 @@ static void launch_main(const BatchParams& bp, const KeyParams& k, hipStream_t s
     }
 }
 
-// Contiguous input, packed output: the stream kernel (salamander_stream.h) unless the
-// wave kernel is forced or the input is not 16-byte aligned (LDS-DMA moves 16-byte
-// chunks); then the stream prepass writes the input offsets and the kernels for
-// explicit offsets run on them.
+// Contiguous input.  Packed output: the wave kernel, which takes the input offsets
+// from a scan of the lengths done with the widths' (tile_sums_kernel,
+// scan_tiles_kernel); the stream kernel (salamander_stream.h) when asked for
+// (HYOBFS_KERNEL_STREAM) and the input is 16-byte aligned (LDS-DMA moves 16-byte
+// chunks).  Slotted output, or wave runs shorter than 64: the stream prepass writes
+// the input offsets and the kernels for explicit offsets run on them.
+// (configs[2], one process: the stream kernel 1.89 ms, the wave kernel on offsets
+// 1.46 ms, profiles/r04_ab_bimodal_*.txt.)
 static bool stream_eligible(const BatchParams& b) {
-    return contiguous_input(b) && b.out_stride == 0 && resolve_kernel(b.kernel) != kKernelWave &&
+    return contiguous_input(b) && b.out_stride == 0 && resolve_kernel(b.kernel) == kKernelStream &&
            (reinterpret_cast<uintptr_t>(b.in) & 15u) == 0;
+}
+static bool wave_scans_input(const BatchParams& b) {   // the wave kernel scans the lengths itself
+    return contiguous_input(b) && b.out_stride == 0 && !stream_eligible(b) && wave_packed_run_log2() == 6;
 }
 
 static uint64_t align16(uint64_t x) { return (x + 15) & ~15ull; }
@@ -206,6 +242,7 @@ uint64_t batch_workspace_bytes(bool obf, const BatchParams& b) {
     const uint64_t tsums = (div_up(b.n, kTile) + 1) * 8;
     if (!contiguous_input(b)) return b.out_stride == 0 ? tsums : 0;
     if (stream_eligible(b)) return stream_workspace_bytes(b.n, b.out_cap, true, false);
+    if (wave_scans_input(b)) return 2 * tsums;
     return align16(stream_workspace_bytes(b.n, 0, false, true)) + (b.out_stride == 0 ? tsums : 0);
 }
 
@@ -215,7 +252,8 @@ int batch_kernel(bool obf, const BatchParams& b) {
     if (stream_eligible(b)) return kKernelStream;
     TileParams T;
     BatchParams bp = b;
-    if (contiguous_input(b)) bp.in_off = reinterpret_cast<const uint64_t*>(16);   // offsets from the prepass
+    if (contiguous_input(b) && !wave_scans_input(b))
+        bp.in_off = reinterpret_cast<const uint64_t*>(16);   // offsets from the prepass
     const bool tile = bp.out_stride != 0 && resolve_kernel(bp.kernel) != kKernelWave &&
                       (obf ? tile_params<true>(bp, T) : tile_params<false>(bp, T));
     return tile ? kKernelTile : kKernelWave;
@@ -239,6 +277,11 @@ static hipError_t launch_contiguous(BatchParams& bp, const KeyParams& k, hipStre
         done = true;
         return hipGetLastError();
     }
+    if (wave_scans_input(bp)) {   // the length sums follow the width sums in the scratch
+        bp.tile_sums = static_cast<uint64_t*>(bp.scratch);
+        bp.in_tile_sums = bp.tile_sums + div_up(bp.n, kTile) + 1;
+        return hipSuccess;
+    }
     launch_stream_prepass<OBF>(bp, S, bp.scratch, false, true, s);
     bp.in_off = S.in_off_out;
     if (bp.out_stride == 0)
@@ -260,13 +303,17 @@ hipError_t launch_salamander(bool obf, const BatchParams& b, const KeyParams& k,
     }
     if (bp.out_stride == 0) {
         if (!bp.tile_sums) return hipErrorInvalidValue;
-        const dim3 grid((uint32_t)ntiles), block(kTile);
+        const dim3 grid((uint32_t)div_up(ntiles, 4)), block(256);
         if (obf)
-            hipLaunchKernelGGL(tile_sums_kernel<true>, grid, block, 0, s, bp);
+            hipLaunchKernelGGL(tile_sums_kernel<true>, grid, block, 0, s, bp, ntiles);
         else
-            hipLaunchKernelGGL(tile_sums_kernel<false>, grid, block, 0, s, bp);
-        hipLaunchKernelGGL(scan_tiles_kernel, dim3(1), dim3(1024), 0, s, bp.tile_sums, ntiles);
+            hipLaunchKernelGGL(tile_sums_kernel<false>, grid, block, 0, s, bp, ntiles);
+        if (bp.in_tile_sums)
+            hipLaunchKernelGGL(scan_tiles_kernel<true>, dim3(1), dim3(1024), 0, s, bp.tile_sums, bp.in_tile_sums, ntiles);
+        else
+            hipLaunchKernelGGL(scan_tiles_kernel<false>, dim3(1), dim3(1024), 0, s, bp.tile_sums, bp.in_tile_sums, ntiles);
         bp.tile_prefix = bp.tile_sums;
+        bp.in_tile_prefix = bp.in_tile_sums;
         if (obf)
             launch_main<true, true>(bp, k, s);
         else

@@ -14,17 +14,18 @@
 //      then per datagram its input and output offset (out_off / out_len) and,
 //      for the datagram holding each tile's first output byte, the tile's
 //      descriptor (that datagram, its offsets, the tile's first input byte);
-//   2. stream kernel: persistent workgroups of four waves walk the tiles.  Per
-//      tile, waves 1-3 copy its input range into LDS by LDS-DMA (one contiguous
-//      range, known from the descriptors alone, 1 KiB per wave instruction,
-//      non-temporal) while wave 0 loads the lengths and salts of the tile's
-//      datagrams and scans them, then all four waves hash the keys, four lanes
-//      per key (quad_key, salamander_tile.h), rotated to the output's 32-byte
-//      phase; after one barrier the chunks that hold a salt or a datagram edge
-//      are assembled and parked in LDS, and all 256 threads sweep the tile's
-//      output in 16-byte chunks (payload bytes from LDS, key XOR, one aligned
-//      non-temporal 16-byte store each).  The descriptors of the workgroup's
-//      next tile are loaded one tile ahead.
+//   2. stream kernel: one workgroup of four waves per tile.  Waves 2-3 copy the
+//      tile's input range into LDS by LDS-DMA (one contiguous range, known from
+//      the descriptors alone, 1 KiB per wave instruction, non-temporal) while
+//      waves 0-1 load the lengths and salts of the tile's datagrams, scan them and
+//      hash the keys, four lanes per key (quad_key, salamander_tile.h), rotated to
+//      the output's 32-byte phase; after one barrier the chunks that hold a salt or
+//      a datagram edge are assembled and parked in LDS, and all 256 threads sweep
+//      the tile's output in 16-byte chunks (payload bytes from LDS, key XOR, one
+//      aligned non-temporal 16-byte store each).  The workgroup exits with its
+//      stores in flight.  (A persistent loop over tiles measured 2.39 ms against
+//      1.48 ms for the wave kernel on configs[2]: each tile's chain started by
+//      waiting for the previous tile's stores, profiles/r04a_ab_bimodal_*.txt.)
 // A tile with more than 64 datagrams runs in passes of 64; a tile whose input
 // span does not fit the LDS stage (long dropped datagrams between its valid
 // ones) reads its payload bytes straight from global memory.  Both are correct
@@ -303,10 +304,19 @@ __device__ __forceinline__ int32_t stream_cand(int32_t o, uint32_t W, int32_t sa
 }
 
 #ifndef HY_STREAM_WAVES
-#define HY_STREAM_WAVES 5   // min waves per SIMD (6 spills at 80 VGPRs; the LDS allows 6 workgroups of 24 KB per CU)
+#define HY_STREAM_WAVES 5   // min waves per SIMD (the LDS allows 6 workgroups of 24 KB per CU)
 #endif
+#ifndef HY_STREAM_LAUNCH_TILES
+#define HY_STREAM_LAUNCH_TILES 65536   // tiles per launch (1 GiB of output): the XCDs stay close in the address space
+#endif
+// One workgroup per output tile (tile t0 + blockIdx.x).  The chain per tile is the
+// uniform tile kernel's: the descriptors, then at once waves 2-3 issue the input
+// window's LDS-DMA while waves 0-1 load lengths and salts, scan and hash the keys;
+// one barrier; boundary chunks; one barrier; the sweep, and the workgroup exits with
+// its stores in flight (no wave ever waits for its own stores).
 template <bool OBF, int SW>
-__global__ __launch_bounds__(256, HY_STREAM_WAVES) void salamander_stream_kernel(BatchParams B, KeyParams K, StreamParams SP) {
+__global__ __launch_bounds__(256, HY_STREAM_WAVES) void salamander_stream_kernel(BatchParams B, KeyParams K,
+                                                                                  StreamParams SP, uint64_t t0) {
     constexpr int32_t SALT = OBF ? 8 : 0;   // salt bytes in front of the output payload
     constexpr int64_t SKIP = OBF ? 0 : 8;   // salt bytes in front of the input payload
     __shared__ __attribute__((aligned(16))) StreamLDS S;
@@ -318,186 +328,178 @@ __global__ __launch_bounds__(256, HY_STREAM_WAVES) void salamander_stream_kernel
     const StreamDesc* __restrict__ D = SP.desc;
     const uint64_t E = D[SP.ntiles_max].o;
     const uint64_t ntiles = (E + kST - 1) / kST;
-    if (blockIdx.x == 0 && tid == 0 && B.out_total) *B.out_total = E;
+    const uint64_t t = t0 + blockIdx.x;
+    if (t == 0 && tid == 0 && B.out_total) *B.out_total = E;
+    if (t >= ntiles) return;
+    // this tile's descriptor and the next one's (or the tail)
+    const StreamDesc* __restrict__ pc = &D[t];
+    const StreamDesc* __restrict__ pn = &D[t + 1 < ntiles ? t + 1 : SP.ntiles_max];
+    const uint64_t d0 = pc->d, s0 = pc->s, o0 = pc->o, in_lo = pc->in0;
+    const uint64_t nd = pn->d, no = pn->o, in_hi = pn->in0;
+    const uint64_t tT = t * kST;
+    const bool last = t + 1 == ntiles;
+    // the tile's datagrams [d0, dend): the next tile's first datagram belongs here
+    // too when it starts inside this tile
+    const uint64_t dend = last ? nd : nd + (no < tT + kST ? 1 : 0);
+    const uint32_t tile_len = (uint32_t)(last ? E - tT : kST);
+    const uint64_t base16 = in_lo & ~15ull;
+    const uint64_t span = ((in_hi + 15) & ~15ull) - base16;
+    const bool staged = span <= kSIn;
 
-    // descriptors of this workgroup's tile t and of t + 1 (or the tail): lanes 0..7
-    auto load_desc = [&](uint64_t t) -> uint64_t {
-        uint64_t v = 0;
-        if (lane < 8 && t < ntiles) {
-            const StreamDesc* p = lane < 4 ? &D[t] : &D[t + 1 < ntiles ? t + 1 : SP.ntiles_max];
-            v = reinterpret_cast<const uint64_t*>(p)[lane & 3];
+    // ---- waves 2-3: the tile's input range into LDS (LDS-DMA, 1 KiB per instruction)
+    if (wid >= 2 && staged) {
+        const uint32_t nch = (uint32_t)(span >> 4);
+        for (uint32_t i = wid - 2; i * 64u < nch; i += 2) {
+            const uint32_t ch = i * 64u + lane;
+            if (ch < nch) glds16(in + base16 + 16u * ch, S.in + kSGuard + 1024u * i);
         }
-        return v;
-    };
-    uint64_t dv = load_desc(blockIdx.x);
-    for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
-        const uint64_t cur = dv;
-        dv = load_desc(t + gridDim.x);   // next tile's, one tile ahead
-        const uint64_t d0 = uni64(__shfl(cur, 0, 64)), s0 = uni64(__shfl(cur, 1, 64));
-        const uint64_t o0 = uni64(__shfl(cur, 2, 64)), in_lo = uni64(__shfl(cur, 3, 64));
-        const uint64_t nd = uni64(__shfl(cur, 4, 64)), no = uni64(__shfl(cur, 6, 64));
-        const uint64_t in_hi = uni64(__shfl(cur, 7, 64));
-        const uint64_t tT = t * kST;
-        const bool last = t + 1 == ntiles;
-        // the tile's datagrams [d0, dend): the next tile's first datagram belongs here
-        // too when it starts inside this tile
-        const uint64_t dend = last ? nd : nd + (no < tT + kST ? 1 : 0);
-        const uint32_t tile_len = (uint32_t)(last ? E - tT : kST);
-        const uint64_t base16 = in_lo & ~15ull;
-        const uint64_t span = ((in_hi + 15) & ~15ull) - base16;
-        const bool staged = span <= kSIn;
-
-        // ---- waves 1-3: the tile's input range into LDS (LDS-DMA, 1 KiB per instruction)
-        if (wid != 0 && staged) {
-            const uint32_t nch = (uint32_t)(span >> 4);
-            for (uint32_t i = wid - 1; i * 64u < nch; i += 3) {
-                const uint32_t ch = i * 64u + lane;
-                if (ch < nch) glds16(in + base16 + 16u * ch, S.in + kSGuard + 1024u * i);
+    }
+    uint64_t sfirst = s0, ofirst = o0;   // offsets of the pass's first datagram
+    for (uint64_t g0 = d0; g0 < dend; g0 += kSD) {
+        const uint32_t mp = (uint32_t)min<uint64_t>((uint64_t)kSD, dend - g0);
+        // ---- every wave: lengths, widths and offsets of the pass's datagrams (lane k:
+        // datagram g0 + k); wave 0 publishes them
+        const uint64_t j = g0 + lane;
+        const bool live = lane < mp;
+        // this wave's key slice: datagram 16 wid + lane / 4 (its salt loads with the lengths)
+        const uint32_t k = 16u * wid + (lane >> 2), qi = lane & 3u;
+        const uint32_t kk = k < mp ? k : 16u * wid;
+        uint64_t salt = 0;
+        if (OBF && 16u * wid < mp) salt = B.salts[g0 + kk];
+        const uint32_t L = live ? B.in_len[j] : 0u;
+        const uint32_t W = live ? out_width<OBF>(L, B.pkt_cap) : 0u;
+        const uint64_t il = wave_incl_scan((uint64_t)L, (int)lane), iw = wave_incl_scan((uint64_t)W, (int)lane);
+        const uint64_t s = sfirst + il - L, o = ofirst + iw - W;
+        sfirst += uni64(__shfl(il, 63, 64));
+        ofirst += uni64(__shfl(iw, 63, 64));
+        if (wid == 0) {
+            S.o[lane] = live ? (int32_t)((int64_t)o - (int64_t)tT) : 0x7FFFFFFF;
+            if (lane == 0) S.o[kSD] = 0x7FFFFFFF;
+            S.w[lane] = W;
+            S.src[lane] = staged ? (int64_t)(s + SKIP) - (int64_t)base16 : (int64_t)(s + SKIP);
+        }
+        // ---- keys: wave w hashes datagrams 16w .. 16w + 15, four lanes each, rotated
+        // to the output phase (key byte of output byte x at x mod 32)
+        if (16u * wid < mp) {
+            if (!OBF) {   // the wire's salt
+                const uint64_t sk = __shfl(s, (int)kk, 64);
+                const uint32_t Wk = __shfl(W, (int)kk, 64);
+                salt = Wk ? load8u(in + sk) : 0;
+            }
+            const uint64_t okk = __shfl(o, (int)kk, 64);
+            const uint64_t kw = quad_key<SW>(K, salt, qi);
+            const uint32_t r = ((uint32_t)okk + (uint32_t)SALT) & 31u;
+            const uint32_t st = (8u * qi - r) & 31u, w0 = st >> 3, sh = (st & 7u) * 8u;
+            const uint64_t a = __shfl(kw, (int)((lane & ~3u) | w0), 64);
+            const uint64_t b = __shfl(kw, (int)((lane & ~3u) | ((w0 + 1) & 3u)), 64);
+            if (k < mp) {
+                S.key[4 * k + qi] = sh ? (a >> sh) | (b << (64 - sh)) : a;
+                if (qi == 0) S.salt[k] = salt;
             }
         }
-        uint64_t sfirst = s0, ofirst = o0;   // offsets of the pass's first datagram (wave 0)
-        for (uint64_t g0 = d0; g0 < dend; g0 += kSD) {
-            const uint32_t mp = (uint32_t)min<uint64_t>((uint64_t)kSD, dend - g0);
-            // ---- wave 0: lengths, offsets, widths, salts of the pass's datagrams into LDS
-            if (wid == 0) {
-                const uint64_t j = g0 + lane;
-                const bool live = lane < mp;
-                const uint32_t L = live ? B.in_len[j] : 0u;
-                const uint32_t W = live ? out_width<OBF>(L, B.pkt_cap) : 0u;
-                const uint64_t il = wave_incl_scan((uint64_t)L, (int)lane), iw = wave_incl_scan((uint64_t)W, (int)lane);
-                const uint64_t s = sfirst + il - L, o = ofirst + iw - W;
-                uint64_t salt = 0;
-                if (OBF) {
-                    if (live) salt = B.salts[j];
-                } else if (W) {
-                    salt = load8u(in + s);   // the wire's salt
-                }
-                S.o[lane] = live ? (int32_t)((int64_t)o - (int64_t)tT) : 0x7FFFFFFF;
-                if (lane == 0) S.o[kSD] = 0x7FFFFFFF;
-                S.w[lane] = W;
-                S.salt[lane] = salt;
-                S.src[lane] = staged ? (int64_t)(s + SKIP) - (int64_t)base16 : (int64_t)(s + SKIP);
-                sfirst = uni64(__shfl(il, 63, 64)) + sfirst;
-                ofirst = uni64(__shfl(iw, 63, 64)) + ofirst;
-            }
-            hy_lds_barrier();
-            // ---- keys: wave w hashes datagrams 16w .. 16w + 15, four lanes each, then
-            // rotates them to the output phase (key byte of output byte x at x mod 32)
-            if (16u * wid < mp) {
-                const uint32_t k = 16u * wid + (lane >> 2), qi = lane & 3u;
-                const uint64_t salt = S.salt[k < mp ? k : 0];
-                const uint64_t kw = quad_key<SW>(K, salt, qi);
-                const uint32_t r = ((uint32_t)S.o[k < mp ? k : 0] + (uint32_t)SALT) & 31u;
-                const uint32_t st = (8u * qi - r) & 31u, w0 = st >> 3, sh = (st & 7u) * 8u;
-                const uint64_t a = __shfl(kw, (int)((lane & ~3u) | w0), 64);
-                const uint64_t b = __shfl(kw, (int)((lane & ~3u) | ((w0 + 1) & 3u)), 64);
-                if (k < mp) S.key[4 * k + qi] = sh ? (a >> sh) | (b << (64 - sh)) : a;
-            }
-            __syncthreads();   // the stage has landed (vmcnt(0)), keys and metadata are published
+        __syncthreads();   // the stage has landed (vmcnt(0) of the DMA waves), keys and metadata are published
 
-            // ---- the pass's output range [ps, pe) (tile-relative); a multi-pass tile
-            // splits at datagram edges, whose partial chunks are stored masked
-            const int32_t ps = g0 == d0 ? 0 : max(S.o[0], 0);
-            int32_t pe = (int32_t)tile_len;
-            if (g0 + mp < dend) pe = S.o[mp - 1] + (int32_t)S.w[mp - 1];
-            const int32_t cA = (ps + 15) >> 4, cB = pe >> 4;   // full chunks [cA, cB)
-            // ---- boundary chunks: wave t (0..2) assembles candidate t of datagram
-            // `lane`, parked when that datagram is the first one touching it
-            if (wid < 3 && lane < mp) {
-                const uint32_t k = lane, W = S.w[k];
-                const int32_t o = S.o[k];
-                uint8_t pk = 0;
-                if (W) {
-                    const int32_t c = stream_cand(o, W, SALT, (int)wid);
-                    bool dup = false;
-                    for (int u = 0; u < (int)wid; ++u) dup = dup || stream_cand(o, W, SALT, u) == c;
-                    const int32_t x = 16 * c;
-                    const bool fast = o + SALT <= x && x + 16 <= o + (int32_t)W;
-                    // the output is contiguous: the previous valid datagram ends at o, so it
-                    // reaches into the chunk unless the chunk starts at or after o
-                    const bool mine = k == 0 || o <= x;
-                    if (!dup && !fast && c >= cA && c < cB && mine) {
-                        u128 rr = 0;
-                        uint32_t cov = 0;
-                        for (uint32_t q = k; q < mp && S.o[q] < x + 16; ++q) stream_contrib<OBF>(S, in, staged, q, x, rr, cov);
-                        if (cov == 0xFFFFu) {
-                            S.park[3 * k + wid] = rr;
-                            pk = 1;
-                        } else if (cov) {
-                            store_masked(B.out + tT + x, rr, cov);
-                        }
-                    }
-                }
-                S.parked[3 * k + wid] = pk;
-            } else if (wid == 3 && lane < 2) {
-                // partial chunks at the pass's ends (multi-pass tiles, the batch's end)
-                const int32_t e0 = (ps & 15) ? (ps >> 4) : -1;
-                int32_t e1 = (pe & 15) ? (pe >> 4) : -1;
-                if (e1 == e0) e1 = -1;
-                const int32_t c = lane == 0 ? e0 : e1;
-                if (c >= 0) {
-                    const int32_t x = 16 * c;
+        // ---- the pass's output range [ps, pe) (tile-relative); a multi-pass tile
+        // splits at datagram edges, whose partial chunks are stored masked
+        const int32_t ps = g0 == d0 ? 0 : max(S.o[0], 0);
+        int32_t pe = (int32_t)tile_len;
+        if (g0 + mp < dend) pe = S.o[mp - 1] + (int32_t)S.w[mp - 1];
+        const int32_t cA = (ps + 15) >> 4, cB = pe >> 4;   // full chunks [cA, cB)
+        // ---- boundary chunks: wave t (0..2) assembles candidate t of datagram
+        // `lane`, parked when that datagram is the first one touching it
+        if (wid < 3 && lane < mp) {
+            const uint32_t k = lane, Wb = S.w[k];
+            const int32_t ob = S.o[k];
+            uint8_t pk = 0;
+            if (Wb) {
+                const int32_t c = stream_cand(ob, Wb, SALT, (int)wid);
+                bool dup = false;
+                for (int u = 0; u < (int)wid; ++u) dup = dup || stream_cand(ob, Wb, SALT, u) == c;
+                const int32_t x = 16 * c;
+                const bool fast = ob + SALT <= x && x + 16 <= ob + (int32_t)Wb;
+                // the output is contiguous: the previous valid datagram ends at ob, so it
+                // reaches into the chunk unless the chunk starts at or after ob
+                const bool mine = k == 0 || ob <= x;
+                if (!dup && !fast && c >= cA && c < cB && mine) {
                     u128 rr = 0;
                     uint32_t cov = 0;
-                    for (uint32_t q = 0; q < mp; ++q)
-                        if (S.o[q] < x + 16) stream_contrib<OBF>(S, in, staged, q, x, rr, cov);
-                    const int32_t lo = max(x, ps), hi = min(x + 16, pe);
-                    cov &= lo < hi ? ((1u << (hi - lo)) - 1u) << (lo - x) : 0u;
-                    if (cov) store_masked(B.out + tT + x, rr, cov);
+                    for (uint32_t q = k; q < mp && S.o[q] < x + 16; ++q) stream_contrib<OBF>(S, in, staged, q, x, rr, cov);
+                    if (cov == 0xFFFFu) {
+                        S.park[3 * k + wid] = rr;
+                        pk = 1;
+                    } else if (cov) {
+                        store_masked(B.out + tT + x, rr, cov);
+                    }
                 }
             }
-            hy_lds_barrier();
+            S.parked[3 * k + wid] = pk;
+        } else if (wid == 3 && lane < 2) {
+            // partial chunks at the pass's ends (multi-pass tiles, the batch's end)
+            const int32_t e0 = (ps & 15) ? (ps >> 4) : -1;
+            int32_t e1 = (pe & 15) ? (pe >> 4) : -1;
+            if (e1 == e0) e1 = -1;
+            const int32_t c = lane == 0 ? e0 : e1;
+            if (c >= 0) {
+                const int32_t x = 16 * c;
+                u128 rr = 0;
+                uint32_t cov = 0;
+                for (uint32_t q = 0; q < mp; ++q)
+                    if (S.o[q] < x + 16) stream_contrib<OBF>(S, in, staged, q, x, rr, cov);
+                const int32_t lo = max(x, ps), hi = min(x + 16, pe);
+                cov &= lo < hi ? ((1u << (hi - lo)) - 1u) << (lo - x) : 0u;
+                if (cov) store_masked(B.out + tT + x, rr, cov);
+            }
+        }
+        hy_lds_barrier();
 
-            // ---- sweep: every full chunk, from LDS (payload XOR key) or from the park
-            uint8_t* __restrict__ ob = B.out + tT;
-            for (int32_t c0 = cA; c0 < cB; c0 += 256 * kSU) {
-                u128 v[kSU];
-                bool ok[kSU];
+        // ---- sweep: every full chunk, from LDS (payload XOR key) or from the park
+        uint8_t* __restrict__ ob = B.out + tT;
+        for (int32_t c0 = cA; c0 < cB; c0 += 256 * kSU) {
+            u128 v[kSU];
+            bool ok[kSU];
 #pragma unroll
-                for (int u = 0; u < kSU; ++u) {
-                    const int32_t c = c0 + u * 256 + (int32_t)tid, x = 16 * c;
-                    ok[u] = false;
-                    v[u] = 0;
-                    if (c >= cB) continue;
-                    uint32_t q = 0;   // last datagram whose output starts at or before x
+            for (int u = 0; u < kSU; ++u) {
+                const int32_t c = c0 + u * 256 + (int32_t)tid, x = 16 * c;
+                ok[u] = false;
+                v[u] = 0;
+                if (c >= cB) continue;
+                uint32_t q = 0;   // last datagram whose output starts at or before x
 #pragma unroll
-                    for (uint32_t step = kSD / 2; step; step >>= 1) q = S.o[q + step] <= x ? q + step : q;
-                    const int32_t oq = S.o[q];
-                    const uint32_t Wq = S.w[q];
-                    if (Wq && oq + SALT <= x && x + 16 <= oq + (int32_t)Wq) {
-                        v[u] = payload16<OBF>(S, in, staged, q, x - (oq + SALT)) ^ key16(S, q, x);
-                        ok[u] = true;
-                    } else {
-                        // the first datagram touching the chunk owns it
-                        uint32_t own = q;
-                        if (!(Wq && oq + (int32_t)Wq > x)) {
-                            own = q + 1;
-                            while (own < mp && S.w[own] == 0) ++own;
-                        }
-                        if (own < mp) {
-                            const int32_t oo = S.o[own];
-                            const uint32_t Wo = S.w[own];
+                for (uint32_t step = kSD / 2; step; step >>= 1) q = S.o[q + step] <= x ? q + step : q;
+                const int32_t oq = S.o[q];
+                const uint32_t Wq = S.w[q];
+                if (Wq && oq + SALT <= x && x + 16 <= oq + (int32_t)Wq) {
+                    v[u] = payload16<OBF>(S, in, staged, q, x - (oq + SALT)) ^ key16(S, q, x);
+                    ok[u] = true;
+                } else {
+                    // the first datagram touching the chunk owns it
+                    uint32_t own = q;
+                    if (!(Wq && oq + (int32_t)Wq > x)) {
+                        own = q + 1;
+                        while (own < mp && S.w[own] == 0) ++own;
+                    }
+                    if (own < mp) {
+                        const int32_t oo = S.o[own];
+                        const uint32_t Wo = S.w[own];
 #pragma unroll
-                            for (int tt = 0; tt < 3; ++tt) {
-                                if (!ok[u] && stream_cand(oo, Wo, SALT, tt) == c && S.parked[3 * own + tt]) {
-                                    v[u] = S.park[3 * own + tt];
-                                    ok[u] = true;
-                                }
+                        for (int tt = 0; tt < 3; ++tt) {
+                            if (!ok[u] && stream_cand(oo, Wo, SALT, tt) == c && S.parked[3 * own + tt]) {
+                                v[u] = S.park[3 * own + tt];
+                                ok[u] = true;
                             }
                         }
                     }
                 }
-#pragma unroll
-                for (int u = 0; u < kSU; ++u) {
-                    const int32_t x = 16 * (c0 + u * 256 + (int32_t)tid);
-                    if (ok[u]) store16_stream(ob + x, v[u]);
-                }
             }
-            // LDS reuse: the next pass / tile overwrites metadata and stage.  Only the LDS
-            // reads must be done (no vmcnt wait): the next tile's DMA goes out while this
-            // tile's stores are still in flight
-            hy_lds_barrier();
+#pragma unroll
+            for (int u = 0; u < kSU; ++u) {
+                const int32_t x = 16 * (c0 + u * 256 + (int32_t)tid);
+                if (ok[u]) store16_stream(ob + x, v[u]);
+            }
         }
+        // a further pass overwrites metadata, keys and parked chunks: only the LDS
+        // reads must be done (no wait for the stores)
+        if (g0 + kSD < dend) hy_lds_barrier();
     }
 }
 
@@ -532,19 +534,13 @@ void launch_stream_prepass(const BatchParams& b, StreamParams& S, void* ws, bool
 
 template <bool OBF, int SW>
 void launch_stream_sw(const BatchParams& b, const KeyParams& k, const StreamParams& S, hipStream_t s) {
-    static const int per_cu = [] {
-        int v = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, salamander_stream_kernel<OBF, SW>, 256, 0) != hipSuccess ||
-            v < 1)
-            v = 1;
-        return v;
-    }();
-    int dev = 0, cus = 0;
-    (void)hipGetDevice(&dev);
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1) cus = 1;
-    const uint64_t cap = (uint64_t)cus * (uint64_t)per_cu;
-    const uint64_t grid = S.ntiles_max < 1 ? 1 : S.ntiles_max < cap ? S.ntiles_max : cap;
-    hipLaunchKernelGGL((salamander_stream_kernel<OBF, SW>), dim3((uint32_t)grid), dim3(256), 0, s, b, k, S);
+    // one workgroup per tile that out_cap allows (tiles past the valid output exit at
+    // once); at least one, which writes out_total
+    const uint64_t nt = S.ntiles_max < 1 ? 1 : S.ntiles_max;
+    for (uint64_t t0 = 0; t0 < nt; t0 += HY_STREAM_LAUNCH_TILES) {
+        const uint64_t g = nt - t0 < (uint64_t)HY_STREAM_LAUNCH_TILES ? nt - t0 : (uint64_t)HY_STREAM_LAUNCH_TILES;
+        hipLaunchKernelGGL((salamander_stream_kernel<OBF, SW>), dim3((uint32_t)g), dim3(256), 0, s, b, k, S, t0);
+    }
 }
 
 }  // namespace hyobfs

@@ -301,10 +301,16 @@ salamander_wave_kernel(BatchParams B, KeyParams K) {
     if (PACKED && RUN == kGroup) {   // tile prefix + widths of the tile's earlier datagrams + wave scan
         const uint64_t p0 = w * DPW;
         const uint64_t tb = p0 / kTile * kTile;
-        uint32_t pre = 0;
-        for (uint64_t q = tb + lane; q < p0; q += kGroup) pre += out_width<OBF>(pkt_len(B, q), B.pkt_cap);
+        uint64_t pre = 0, ipre = 0;   // widths and (contiguous input) lengths of the tile's earlier datagrams
+        for (uint64_t q = tb + lane; q < p0; q += kGroup) {
+            const uint32_t Lq = pkt_len(B, q);
+            pre += out_width<OBF>(Lq, B.pkt_cap);
+            ipre += Lq;
+        }
         rfirst = uni64(B.tile_prefix[p0 / kTile] + wave_sum(pre));
         ooff = rfirst + wave_incl_scan(W, lane) - W;
+        if (B.in_tile_prefix)   // contiguous input: offsets from the scan of the lengths
+            ioff = uni64(B.in_tile_prefix[p0 / kTile] + wave_sum(ipre)) + wave_incl_scan((uint64_t)L, lane) - L;
     } else if (PACKED) {   // shorter runs: the same per run, over the run's RUN lanes
         const uint64_t s0 = r << rl;   // the run's first datagram
         const uint64_t tb = s0 / kTile * kTile;

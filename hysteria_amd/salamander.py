@@ -136,11 +136,12 @@ class SalamanderObfuscator:
     def __exit__(self, *exc):
         self.close()
 
-    KERNELS = {"auto": 0, "wave": 1, "tile": 2}
+    KERNELS = {"auto": 0, "wave": 1, "tile": 2, "stream": 3}
 
     def set_kernel(self, kernel: str) -> None:
         """Batch kernel of this context: "auto" (the tile kernel where it applies, else the
-        wave-group kernel), "wave" (forced) or "tile" (include/hyobfs.h, HYOBFS_KERNEL_*)."""
+        wave-group kernel), "wave" (forced), "tile" or "stream" (contiguous packed input:
+        the stream kernel; include/hyobfs.h, HYOBFS_KERNEL_*)."""
         check(self._lib.hyobfs_salamander_set_kernel(self._h, self.KERNELS[kernel]), "set_kernel")
         self.kernel = kernel
 

@@ -112,15 +112,18 @@ int hyobfs_salamander_device(const hyobfs_salamander* ctx);
    payloads of 16 bytes or more, nothing dropped, no 16-byte chunk holding two
    datagrams' payload bytes) -- the uniform 1200-byte batch of the benchmark --
    and the wave-group kernel on every other batch (packed output, ragged
-   lengths, any alignment).  HYOBFS_KERNEL_WAVE forces the wave-group kernel;
-   HYOBFS_KERNEL_TILE is AUTO.  The HYOBFS_KERNEL environment variable
-   (wave|tile) overrides AUTO.  Returns HYOBFS_ERR_INVALID for an unknown value.
-   Outputs are identical. */
+   lengths, any alignment; contiguous input scans its lengths alongside the
+   widths).  HYOBFS_KERNEL_WAVE forces the wave-group kernel; HYOBFS_KERNEL_TILE
+   is AUTO; HYOBFS_KERNEL_STREAM runs the stream kernel on contiguous input with
+   packed output and a 16-byte aligned `in` (AUTO elsewhere; slower than AUTO on
+   the benchmark's mix today, kept for tuning).  The HYOBFS_KERNEL environment
+   variable (wave|tile|stream) overrides AUTO.  Returns HYOBFS_ERR_INVALID for an
+   unknown value.  Outputs are identical. */
 enum {
     HYOBFS_KERNEL_AUTO = 0,
     HYOBFS_KERNEL_WAVE = 1,
     HYOBFS_KERNEL_TILE = 2,
-    HYOBFS_KERNEL_STREAM = 3   /* reported by hyobfs_salamander_batch_kernel only */
+    HYOBFS_KERNEL_STREAM = 3
 };
 int hyobfs_salamander_set_kernel(hyobfs_salamander* ctx, int kernel);
 
@@ -207,9 +210,11 @@ typedef struct hyobfs_batch {
 /* Scratch of a packed batch with explicit or strided input offsets: (ceil(n/256)+1) x 8. */
 uint64_t hyobfs_batch_workspace_size(uint64_t n);
 /* Scratch any batch needs, whatever the kernel choice: the above for packed
-   batches with explicit offsets; for contiguous input the stream prepass's
-   block sums (16 B per 1024 datagrams), tile descriptors (32 B per 16 KiB of
-   out_cap) or input offsets (8 B per datagram); 0 for slotted batches. */
+   batches with explicit offsets; for contiguous input with packed output twice
+   that (width and length sums) or, for the stream kernel, its prepass's block
+   sums (16 B per 1024 datagrams) and tile descriptors (32 B per 16 KiB of
+   out_cap); slotted output with contiguous input: input offsets (8 B per
+   datagram); 0 for other slotted batches. */
 uint64_t hyobfs_batch_workspace_bytes(const hyobfs_batch* b);
 /* Which batch kernel a call with this batch would run under the context's
    setting (HYOBFS_KERNEL_TILE, _WAVE or _STREAM; HYOBFS_KERNEL_AUTO for an

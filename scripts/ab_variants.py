@@ -10,7 +10,8 @@ A name ending in "!" is an ablation build (wrong output): its wire is not checke
 AB_WORKLOAD=bimodal runs BASELINE configs[2] instead (P datagrams of the 40 % 64 B /
 60 % 1350 B mix, default 4M, packed output).  Bimodal input is contiguous (in_off NULL:
 the stream kernel under auto); a kernel name with "@off" passes explicit in_off /
-out_off arrays instead (the round-3 layout: the wave kernel).
+out_off arrays instead (the round-3 layout: the wave kernel).  AB_LEN_MAP="1350:1344"
+replaces lengths (alignment studies).
 """
 import os
 import statistics
@@ -34,6 +35,9 @@ if WL == "bimodal":
     P = int(sys.argv[3]) if len(sys.argv) > 3 else 1 << 22
     lens = torch.empty(P, dtype=torch.int32, device=dev)
     hysteria_amd.synth_bimodal_lengths(lens, P, 3, 0)
+    for kv in filter(None, os.environ.get("AB_LEN_MAP", "").split(",")):   # e.g. 1350:1352 (alignment study)
+        x, y = (int(v) for v in kv.split(":"))
+        lens[lens == x] = y
     in_off = torch.zeros(P, dtype=torch.int64, device=dev)
     in_off[1:] = torch.cumsum(lens[:-1].to(torch.int64), 0)
     total_in = int(lens.to(torch.int64).sum())

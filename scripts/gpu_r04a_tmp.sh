@@ -1,5 +1,6 @@
 set -u
-bash scripts/gpu_session.sh r04a test || exit 1
-AB_WORKLOAD=bimodal AB_ARGS="auto,auto@off,wave" AB_NAME=bimodal_layouts bash scripts/gpu_session.sh r04a ab bench trace || exit 1
-AB_WORKLOAD=bimodal AB_ARGS="auto" AB_NAME=bimodal_variants AB_LIBS=main=hysteria_amd/libhyobfs.so,s4u4=build_variants/libhyobfs_s4u4.so,s6u2=build_variants/libhyobfs_s6u2.so,t32=build_variants/libhyobfs_t32.so,t8=build_variants/libhyobfs_t8.so bash scripts/gpu_session.sh r04a ab || exit 1
-AB_NAME=gecko bash scripts/gpu_session.sh r04a abg aux pmc:main:uniform_deobf:FETCH_SIZE pmc:saltt:uniform_deobf:FETCH_SIZE || exit 1
+bash scripts/gpu_session.sh r04j test:contig || exit 1
+AB_WORKLOAD=bimodal AB_ARGS="auto,auto@off" AB_NAME=bimodal_prepass AB_LIBS='main=hysteria_amd/libhyobfs.so' bash scripts/gpu_session.sh r04j ab || exit 1
+R=$GRAFT_REPO_ROOT
+(cd /tmp && export TMPDIR=/tmp && timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/r04j/trace_bimodal -o run -- python3 $R/scripts/prof_one.py bimodal 10 > $R/gpurun_out/r04j/trace_bimodal.log 2>&1) || exit 1
+bash scripts/gpu_session.sh r04j pmc:main:uniform:FETCH_SIZE pmc:saltt:uniform:FETCH_SIZE bench || exit 1

@@ -25,12 +25,13 @@ TAG=${1:?tag}
 shift
 O=$R/gpurun_out/$TAG
 mkdir -p "$O"
+exec 3>&1   # step markers go to the session's stdout, not into a step's redirected output
 step() {
   local name=$1 lim=$2; shift 2
-  echo "== $name $(date +%T)"
+  echo "== $name $(date +%T)" >&3
   timeout -k 10 "$lim" "$@"
   local rc=$?
-  echo "== $name rc=$rc"
+  echo "== $name rc=$rc" >&3
   [ $rc -eq 0 ] || exit $rc
 }
 for s in "$@"; do

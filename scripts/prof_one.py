@@ -9,6 +9,8 @@ import torch, hysteria_amd
 wl = sys.argv[1] if len(sys.argv) > 1 else "uniform"
 K = int(sys.argv[2]) if len(sys.argv) > 2 else 5
 kern = sys.argv[3] if len(sys.argv) > 3 else "auto"
+if wl not in ("uniform", "bimodal", "bimodal_off"):
+    sys.exit(f"unknown workload {wl!r}: uniform | bimodal | bimodal_off")
 dev = torch.device("cuda:0")
 o = hysteria_amd.SalamanderObfuscator(b"average_password", 0)
 o.set_kernel(kern)
@@ -41,7 +43,7 @@ else:
     for _ in range(K):
         o.obfuscate_batch(inp, P, in_off=in_off, in_len=lens, salts=salts, out=wire, out_cap=cap,
                           out_off=out_off, out_len=out_len, workspace=ws, workspace_bytes=ws.numel())
-    for _ in range(K):
+    for _ in range(K if os.environ.get("PROF_ORDER") != "deobf_last_obf" else 0):
         o.deobfuscate_batch(wire, P, in_off=None if in_off is None else out_off, in_len=out_len, out=back, out_cap=total_in,
                             workspace=ws, workspace_bytes=ws.numel())
 torch.cuda.synchronize()

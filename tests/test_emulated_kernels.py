@@ -46,9 +46,10 @@ SPECS = {
                                 "HYOBFS_KERNEL": "wave"}),
     "test_emulated_kernel_vs_oracle": lambda p: (p["which"], p["args"], {"HYEMU_CUS": p["cus"]}),
     "test_emulated_split_launches": lambda p: (p["which"], p["args"], dict(p["env"])),
-    "test_emulated_stream_kernel": lambda p: ("contig", p["args"], {"HYEMU_CUS": "2"}),
-    "test_emulated_contiguous_input_wave_forced": lambda p: ("contig", p["args"], {"HYEMU_CUS": "2",
-                                                                                   "HYOBFS_KERNEL": "wave"}),
+    "test_emulated_stream_kernel": lambda p: ("contig", p["args"], {"HYEMU_CUS": "2", "HYOBFS_KERNEL": "stream"}),
+    "test_emulated_contiguous_input_auto": lambda p: ("contig", p["args"], {"HYEMU_CUS": "2"}),
+    "test_emulated_contiguous_input_prepass_offsets": lambda p: ("contig", p["args"], {
+        "HYEMU_CUS": "2", "HYOBFS_PACKED_RUN_LOG2": "3"}),
 }
 
 
@@ -149,12 +150,14 @@ PACKED_CASES = [
 ]
 
 
-# Contiguous packed input (in_off NULL, in_stride 0) into packed output: the stream
-# kernel (salamander_stream.h) under AUTO, the prepass's input offsets + wave kernel when
-# forced (tests/emu/run_case.py case_contig: seed n dist obf cap% psk_len [pkt_cap misalign]).
-# Bimodal, 0..2100 B, tiny (multi-pass tiles, several datagrams per chunk), 1-5 KB,
-# zero-length datagrams; out_cap cuts, pkt_cap drops, real wire with 8-byte datagrams,
-# PSKs across salt words and the two-block case, a misaligned input (the fallback).
+# Contiguous packed input (in_off NULL, in_stride 0) into packed output
+# (tests/emu/run_case.py case_contig: seed n dist obf cap% psk_len [pkt_cap misalign]):
+# AUTO = the wave kernel taking its input offsets from the scan of the lengths;
+# HYOBFS_KERNEL=stream the stream kernel (salamander_stream.h); wave runs of 8 the
+# stream prepass's input offsets.  Bimodal, 0..2100 B, tiny (multi-pass tiles, several
+# datagrams per chunk), 1-5 KB, zero-length datagrams; out_cap cuts, pkt_cap drops,
+# real wire with 8-byte datagrams, PSKs across salt words and the two-block case, a
+# misaligned input.
 CONTIG_CASES = [
     "1 3000 0 1 100 16", "2 3000 0 0 100 16", "3 2000 1 1 100 16", "4 2000 1 0 100 33", "5 3000 2 1 100 16",
     "6 3000 2 0 100 121", "7 300 3 1 100 16", "8 300 3 0 100 4", "9 3000 4 1 100 16", "10 3000 4 0 100 16",
@@ -165,12 +168,17 @@ CONTIG_CASES = [
 
 @pytest.mark.parametrize("args", CONTIG_CASES)
 def test_emulated_stream_kernel(emu_lib, args):
+    _run(emu_lib, "contig", args, {"HYEMU_CUS": "2", "HYOBFS_KERNEL": "stream"})
+
+
+@pytest.mark.parametrize("args", CONTIG_CASES)
+def test_emulated_contiguous_input_auto(emu_lib, args):
     _run(emu_lib, "contig", args, {"HYEMU_CUS": "2"})
 
 
-@pytest.mark.parametrize("args", CONTIG_CASES[:6] + CONTIG_CASES[10:12])
-def test_emulated_contiguous_input_wave_forced(emu_lib, args):
-    _run(emu_lib, "contig", args, {"HYEMU_CUS": "2", "HYOBFS_KERNEL": "wave"})
+@pytest.mark.parametrize("args", CONTIG_CASES[:4] + CONTIG_CASES[10:12])
+def test_emulated_contiguous_input_prepass_offsets(emu_lib, args):
+    _run(emu_lib, "contig", args, {"HYEMU_CUS": "2", "HYOBFS_PACKED_RUN_LOG2": "3"})
 
 
 @pytest.mark.parametrize("which,args", PACKED_CASES)

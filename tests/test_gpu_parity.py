@@ -367,18 +367,29 @@ def test_config3_bimodal_4M_digest(obfs, gpu, golden):
     assert h.hexdigest() == d["obf_sha256"]
 
 
-# ------------------------------------------- contiguous input: the stream kernel
+# ------------------------------------------- contiguous input: wave scan / stream kernel
+@pytest.fixture(params=["auto", "stream", "wave"])
+def contig_obfs(gpu, request):
+    """auto and wave: the wave kernel scanning the input lengths with the widths;
+    stream: the stream kernel (salamander_stream.h)."""
+    import hysteria_amd
+    o = hysteria_amd.SalamanderObfuscator(PSK, 0)
+    o.set_kernel(request.param)
+    yield o
+    o.close()
+
+
 def _stream_expected(obfs):
-    return "wave" if getattr(obfs, "kernel", "auto") == "wave" else "stream"
+    return "stream" if obfs.kernel == "stream" else "wave"
 
 
-def test_contiguous_bimodal_64k_vs_oracle_and_digest(obfs, gpu, coracle, golden):
+def test_contiguous_bimodal_64k_vs_oracle_and_digest(contig_obfs, gpu, coracle, golden):
     """Contiguous packed input (in_off NULL, in_stride 0: datagram i right after
-    datagram i-1, include/hyobfs.h) into packed output: the stream kernel
-    (salamander_stream.h) under auto, the prepass's offsets + wave kernel under wave.
+    datagram i-1, include/hyobfs.h) into packed output, under each kernel choice.
     The wire equals the explicit-offset batch's (the committed digest and the C
     oracle byte for byte); the wire, itself contiguous, deobfuscates back."""
     import torch
+    obfs = contig_obfs
     d = golden[1]["bimodal_64k"]
     n = d["n"]
     lens, in_off, inp, salts, total_in = _bimodal(gpu, n)
@@ -409,10 +420,11 @@ def test_contiguous_bimodal_64k_vs_oracle_and_digest(obfs, gpu, coracle, golden)
     assert (hb[total_in:] == 0x5A).all() and int(_host(total)[0]) == total_in
 
 
-def test_contiguous_config3_4M_digest_and_roundtrip(obfs, gpu, golden):
+def test_contiguous_config3_4M_digest_and_roundtrip(contig_obfs, gpu, golden):
     """BASELINE configs[2] at full size through the contiguous layout (what bench.py runs):
     the committed 4M digest, and the device round trip."""
     import torch
+    obfs = contig_obfs
     d = golden[1]["config3_bimodal_4M"]
     n = d["n"]
     lens, in_off, inp, salts, total_in = _bimodal(gpu, n)
@@ -444,9 +456,9 @@ CONTIG_GPU = [(1, 20000, 0, 1, 100, 16, 0, 0), (2, 20000, 0, 0, 100, 16, 0, 0), 
 
 
 @pytest.mark.parametrize("case", CONTIG_GPU)
-def test_contiguous_input_grid_vs_oracle(obfs, gpu, coracle, case):
-    """The stream kernel's edge cases byte for byte against the C oracle, sentinel bytes
-    past the output: tiles with more than 64 datagrams and several per 16-byte chunk,
+def test_contiguous_input_grid_vs_oracle(contig_obfs, gpu, coracle, case):
+    """The contiguous layout's edge cases under each kernel choice, byte for byte against
+    the C oracle, sentinel bytes past the output: tiles with more than 64 datagrams and several per 16-byte chunk,
     zero-length datagrams, out_cap cuts (the tail), pkt_cap drops (holes in the input),
     real wire with 8-byte datagrams, PSKs across salt words and two blocks, misaligned
     input (the offsets + wave kernel fallback)."""
@@ -481,10 +493,14 @@ def test_contiguous_input_grid_vs_oracle(obfs, gpu, coracle, case):
               out_total=tot)
     if obf:
         kw["salts"] = _u64(salts, gpu)
-    want = "wave" if mis or getattr(obfs, "kernel", "auto") == "wave" else "stream"
-    assert obfs.batch_kernel(bool(obf), inp=src, n=n, **kw) == want
-    (obfs.obfuscate_batch if obf else obfs.deobfuscate_batch)(inp=src, n=n, **kw)
-    got = _host(out)
+    import hysteria_amd
+    kern = contig_obfs.kernel
+    want = "stream" if kern == "stream" and not mis else "wave"
+    with hysteria_amd.SalamanderObfuscator(psk, 0) as o:   # the case's PSK (the fixture's is average_password)
+        o.set_kernel(kern)
+        assert o.batch_kernel(bool(obf), inp=src, n=n, **kw) == want
+        (o.obfuscate_batch if obf else o.deobfuscate_batch)(inp=src, n=n, **kw)
+        got = _host(out)
     assert np.array_equal(_host(out_off).view(np.uint64), eoff)
     assert np.array_equal(_host(out_len).view(np.uint32), elen)
     assert int(_host(tot)[0]) == etot
