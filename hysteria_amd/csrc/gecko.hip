@@ -534,7 +534,7 @@ __global__ __launch_bounds__(256) HY_GK_ATTR void gecko_encode_kernel(KeyParams 
 // When the caller gives out_cap and every frame is valid and lies after the one
 // before it (back to back or with gaps: what writeFragmented and plan_fragments
 // produce), the wire is cut into tiles of kGT bytes, 128-byte aligned, and
-// persistent workgroups walk them: wave 0 loads the records of the frames that
+// one workgroup per tile: wave 0 loads the records of the frames that
 // touch the tile, all four waves hash their keys (four lanes per key, quad_key of
 // salamander_tile.h) and rotate them to the wire phase, the chunks holding a frame's
 // salt, header, padding/chunk seam or end are assembled once (gk_contrib) and parked,
@@ -591,7 +591,8 @@ __global__ __launch_bounds__(256) void gecko_tiles_kernel(hyobfs_gecko_batch B, 
 }
 
 template <int SW>
-__global__ __launch_bounds__(256) HY_GK_ATTR void gecko_tile_kernel(KeyParams K, hyobfs_gecko_batch B, GkTiles S) {
+__global__ __launch_bounds__(256) HY_GK_ATTR void gecko_tile_kernel(KeyParams K, hyobfs_gecko_batch B, GkTiles S,
+                                                                    uint64_t t0) {
     __shared__ GeckoGroup G;
     __shared__ gk_u128 s_park[kGC * 64];
     __shared__ uint8_t s_parked[kGC * 64];
@@ -601,7 +602,10 @@ __global__ __launch_bounds__(256) HY_GK_ATTR void gecko_tile_kernel(KeyParams K,
     const uint64_t E = uni64(*S.end);
     const uint64_t ntiles = (E + kGT - 1) / kGT;
     const GkPad P = gk_pad_params(B);
-    for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    // one workgroup per wire tile (a persistent loop over tiles made every tile wait
+    // for the previous one's stores: 1.35 ms against 0.57 for the wave-group kernel)
+    const uint64_t t = t0 + blockIdx.x;
+    if (t < ntiles) {
         const uint64_t tT = t * kGT;
         const uint64_t base = tT >= kGTBack ? tT - kGTBack : 0;
         const uint32_t xo = (uint32_t)(tT - base);                          // the tile's start, group-relative
@@ -790,17 +794,14 @@ uint64_t gecko_tiles_workspace_bytes(uint64_t out_cap) {
 
 template <int SW>
 static void launch_gecko_tile_sw(const KeyParams& k, const hyobfs_gecko_batch& b, const GkTiles& S, hipStream_t s) {
-    static const int per_cu = [] {
-        int v = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, gecko_tile_kernel<SW>, 256, 0) != hipSuccess || v < 1) v = 1;
-        return v;
-    }();
-    int dev = 0, cus = 0;
-    (void)hipGetDevice(&dev);
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1) cus = 1;
-    const uint64_t cap = (uint64_t)cus * (uint64_t)per_cu;
-    const uint64_t grid = S.ntiles_max < 1 ? 1 : S.ntiles_max < cap ? S.ntiles_max : cap;
-    hipLaunchKernelGGL(gecko_tile_kernel<SW>, dim3((uint32_t)grid), dim3(256), 0, s, k, b, S);
+    // one workgroup per tile out_cap allows (those past the wire's end exit at once),
+    // launches of at most 65536 tiles (1 GiB of wire)
+    constexpr uint64_t kLaunch = 65536;
+    const uint64_t nt = S.ntiles_max < 1 ? 1 : S.ntiles_max;
+    for (uint64_t t0 = 0; t0 < nt; t0 += kLaunch) {
+        const uint64_t g = nt - t0 < kLaunch ? nt - t0 : kLaunch;
+        hipLaunchKernelGGL(gecko_tile_kernel<SW>, dim3((uint32_t)g), dim3(256), 0, s, k, b, S, t0);
+    }
 }
 
 hipError_t launch_gecko_encode(const KeyParams& k, const hyobfs_gecko_batch& b, void* ws, hipStream_t s) {

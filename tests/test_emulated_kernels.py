@@ -171,12 +171,17 @@ def test_emulated_stream_kernel(emu_lib, args):
     _run(emu_lib, "contig", args, {"HYEMU_CUS": "2", "HYOBFS_KERNEL": "stream"})
 
 
-@pytest.mark.parametrize("args", CONTIG_CASES)
+# AUTO: the cases whose layout differs for the wave kernel's length scan (bimodal, ragged,
+# tiny, zero lengths, cuts, drops, two-block PSK, misaligned input)
+CONTIG_AUTO = [CONTIG_CASES[i] for i in (0, 1, 2, 4, 8, 10, 11, 13, 14)]
+
+
+@pytest.mark.parametrize("args", CONTIG_AUTO)
 def test_emulated_contiguous_input_auto(emu_lib, args):
     _run(emu_lib, "contig", args, {"HYEMU_CUS": "2"})
 
 
-@pytest.mark.parametrize("args", CONTIG_CASES[:4] + CONTIG_CASES[10:12])
+@pytest.mark.parametrize("args", [CONTIG_CASES[i] for i in (1, 2, 10)])
 def test_emulated_contiguous_input_prepass_offsets(emu_lib, args):
     _run(emu_lib, "contig", args, {"HYEMU_CUS": "2", "HYOBFS_PACKED_RUN_LOG2": "3"})
 
