@@ -699,7 +699,10 @@ int hyobfs_gecko_encode_batch(hyobfs_salamander* c, const hyobfs_gecko_batch* b,
     bool zero_key = true;
     for (int i = 0; i < 32; ++i) zero_key = zero_key && b->pad_key[i] == 0;
     if (zero_key) return HYOBFS_ERR_INVALID;
-    const uint64_t ws_need = hyobfs_gecko_workspace_bytes(b);
+    // the wire-tile kernel only when asked for (HYOBFS_KERNEL_STREAM): on the benchmark's
+    // frames it is slower than the wave-group kernel (profiles/r04_abg_gecko_*.txt)
+    const bool tiles = hyobfs::resolve_kernel(c->kernel) == hyobfs::kKernelStream;
+    const uint64_t ws_need = tiles ? hyobfs_gecko_workspace_bytes(b) : 0;
     if (ws_need && b->workspace && b->workspace_bytes < ws_need) return HYOBFS_ERR_INVALID;
     DeviceGuard g(c->device);
     if (!g.ok) return HYOBFS_ERR_HIP;
@@ -712,7 +715,7 @@ int hyobfs_gecko_encode_batch(hyobfs_salamander* c, const hyobfs_gecko_batch* b,
         if (hipMallocFromPoolAsync(&scratch, ws_need, pool, s) != hipSuccess) return HYOBFS_ERR_NOMEM;
         ws = scratch;
     }
-    const hipError_t e = hyobfs::launch_gecko_encode(c->kp, *b, ws, s);
+    const hipError_t e = hyobfs::launch_gecko_encode(c->kp, *b, tiles ? ws : nullptr, s);
     if (scratch && hipFreeAsync(scratch, s) != hipSuccess) return HYOBFS_ERR_HIP;
     return e == hipSuccess ? HYOBFS_OK : HYOBFS_ERR_HIP;
 }

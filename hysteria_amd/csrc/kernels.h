@@ -89,6 +89,7 @@ inline bool contiguous_input(const BatchParams& b) { return !b.in_off && b.in_st
 hipError_t launch_keys(const KeyParams& k, const uint64_t* salts, uint8_t* keys, uint64_t n,
                        hipStream_t s);
 // ws: gecko_tiles_workspace_bytes(b.out_cap) bytes (NULL or out_cap 0: the wave-group kernel only)
+// ws: the wire-tile kernel's scratch (gecko_tiles_workspace_bytes), NULL = the wave-group kernel
 hipError_t launch_gecko_encode(const KeyParams& k, const hyobfs_gecko_batch& b, void* ws, hipStream_t s);
 uint64_t gecko_tiles_workspace_bytes(uint64_t out_cap);
 hipError_t launch_gecko_parse(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint64_t n,

@@ -39,9 +39,14 @@ doff = torch.from_numpy(off.view(np.uint8)).to(dev)
 alg = M * L + total
 modes = os.environ.get("AB_GK_MODES", "tile,wave").split(",")
 ws = torch.empty(max(16, gecko.workspace_bytes(out.numel())), dtype=torch.uint8, device=dev)
-obs = {name: hysteria_amd.SalamanderObfuscator(b"average_password", 0, lib_path=path) for name, path in libs}
+obs = {}
+for name, path in libs:
+    for m in modes:
+        o = hysteria_amd.SalamanderObfuscator(b"average_password", 0, lib_path=path)
+        if m == "tile":
+            o.set_kernel("stream")   # the wire-tile kernel is opt-in
+        obs[f"{name}/{m}"] = o
 libs = [(f"{name}/{m}", path) for name, path in libs for m in modes]
-obs = {f"{name}/{m}": o for name, o in obs.items() for m in modes}
 
 
 def run(name):

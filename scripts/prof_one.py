@@ -1,16 +1,17 @@
 """Minimal driver for rocprofv3 counter passes: K obfuscate + K deobfuscate launches
 of the uniform 1M x 1200 B batch (BASELINE configs[1]), or of the 4M bimodal
 batch (configs[2], packed output) with 'bimodal' (contiguous input, as bench.py) or
-'bimodal_off' (explicit offsets).  Optional 3rd argument: the context's kernel
-(auto|wave|persistent|uniform)."""
+'bimodal_off' (explicit offsets); 'bimodal_alt': 20 warm-up obfuscate launches, then
+K of each layout alternating (obfuscate only).  Optional 3rd argument: the context's
+kernel (auto|wave|tile|stream)."""
 import os, sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch, hysteria_amd
 wl = sys.argv[1] if len(sys.argv) > 1 else "uniform"
 K = int(sys.argv[2]) if len(sys.argv) > 2 else 5
 kern = sys.argv[3] if len(sys.argv) > 3 else "auto"
-if wl not in ("uniform", "bimodal", "bimodal_off"):
-    sys.exit(f"unknown workload {wl!r}: uniform | bimodal | bimodal_off")
+if wl not in ("uniform", "bimodal", "bimodal_off", "bimodal_alt"):
+    sys.exit(f"unknown workload {wl!r}: uniform | bimodal | bimodal_off | bimodal_alt")
 dev = torch.device("cuda:0")
 o = hysteria_amd.SalamanderObfuscator(b"average_password", 0)
 o.set_kernel(kern)
@@ -27,7 +28,7 @@ else:
     P = 1 << 22
     lens = torch.empty(P, dtype=torch.int32, device=dev); hysteria_amd.synth_bimodal_lengths(lens, P, 3, 0)
     in_off = None
-    if wl == "bimodal_off":
+    if wl in ("bimodal_off", "bimodal_alt"):
         in_off = torch.zeros(P, dtype=torch.int64, device=dev); in_off[1:] = torch.cumsum(lens[:-1].to(torch.int64), 0)
     total_in = int(lens.to(torch.int64).sum())
     inp = torch.empty(total_in + 16, dtype=torch.uint8, device=dev); hysteria_amd.synth_stream(inp, total_in, 1, 0)
@@ -40,6 +41,11 @@ else:
     nws = max(o.workspace_bytes(inp=inp, n=P, in_off=in_off, in_len=lens, out=wire, out_cap=cap),
               o.workspace_bytes(inp=wire, n=P, in_off=None if in_off is None else out_off, in_len=out_len, out=back, out_cap=total_in))
     ws = torch.empty(max(nws, 16), dtype=torch.uint8, device=dev)
+    if wl == "bimodal_alt":   # 20 warm-up launches, then contiguous and explicit offsets alternating
+        for i in range(20 + 2 * K):
+            o.obfuscate_batch(inp, P, in_off=in_off if i % 2 else None, in_len=lens, salts=salts, out=wire,
+                              out_cap=cap, out_off=out_off, out_len=out_len, workspace=ws, workspace_bytes=ws.numel())
+        K = 0
     for _ in range(K):
         o.obfuscate_batch(inp, P, in_off=in_off, in_len=lens, salts=salts, out=wire, out_cap=cap,
                           out_off=out_off, out_len=out_len, workspace=ws, workspace_bytes=ws.numel())

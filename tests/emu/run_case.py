@@ -272,6 +272,8 @@ def case_gecko(n_msgs, seed, layout=0, tiles=1):
     salts = ref.splitmix64_array(5, 0, nf)
     out = np.full(total + 64, 0xA5, np.uint8)
     o = SalamanderObfuscator(psk, 0)
+    if tiles:
+        o.set_kernel("stream")   # the wire-tile kernel is opt-in
     p = lambda a: a.ctypes.data  # noqa: E731
     key, nonce = bytes(range(3, 35)), bytes(range(40, 52))
     # out_cap given: frames in order run the wire-tile kernel (layouts 0, 1, 3), shuffled

@@ -34,8 +34,8 @@ def _messages(n, seed):
                                           (3000, 512, 1200)])
 def test_encode_batch_vs_oracle(gpu, n_msgs, lo, hi, tiles):
     """Device frames byte for byte against oracle/gecko_ref.py: through the wire-tile
-    kernel (out_cap given, frames in wire order; asserted through the workspace's flag)
-    and through the wave-group kernel (no out_cap)."""
+    kernel (context kernel "stream", out_cap given, frames in wire order; asserted
+    through the workspace's flag) and through the wave-group kernel (the default)."""
     import torch
     import hysteria_amd
     from hysteria_amd import gecko
@@ -44,6 +44,8 @@ def test_encode_batch_vs_oracle(gpu, n_msgs, lo, hi, tiles):
     nf = len(fr)
     salts = sref.splitmix64_array(5, 0, nf)
     o = hysteria_amd.SalamanderObfuscator(PSK, 0)
+    if tiles:
+        o.set_kernel("stream")   # the wire-tile kernel is opt-in (HYOBFS_KERNEL_STREAM)
     try:
         out = torch.full((total + 64,), 0xA5, dtype=torch.uint8, device=gpu)
         cap = total + 64 if tiles else 0
