@@ -63,85 +63,65 @@ __global__ __launch_bounds__(256) void tile_sums_kernel(BatchParams B, uint64_t 
     }
 }
 
-// Exclusive scan of ntiles values in place -- of v, and of v2 when given
-// (contiguous input: the length sums) -- one workgroup of 1024 threads; writes
-// the totals at [ntiles].  A pass covers 8192 values per array: wave w owns 512
+// Exclusive scan of ntiles values in place, one workgroup of 1024 threads per
+// array: workgroup 0 scans v, workgroup 1 (contiguous input) the length sums v2;
+// each writes its total at [ntiles].  A pass covers 8192 values: wave w owns 512
 // consecutive ones, loaded and stored coalesced (64 lanes x 8 B per instruction)
 // and transposed through LDS so that lane l sums values 8l .. 8l + 7 of the wave's
 // block sequentially.  (Loading each thread's 16 consecutive values directly --
 // one cache line per lane -- took 20 us per array for 16384 tiles on the one CU
-// that runs this.)
-template <bool TWO>
+// that runs this; this takes 12.)
 __global__ __launch_bounds__(1024) void scan_tiles_kernel(uint64_t* v, uint64_t* v2, uint64_t ntiles) {
-    constexpr int PER = 8, NA = TWO ? 2 : 1, BLK = 64 * PER;
-    constexpr int PAD = PER + 1;                 // LDS row of a lane: PER values + 1 (fewer bank conflicts)
-    __shared__ uint64_t s_x[NA][16][64 * PAD];   // per array, per wave: the block, lane-major
-    __shared__ uint64_t s_w[NA][16];
-    __shared__ uint64_t s_carry[NA];
+    constexpr int PER = 8, BLK = 64 * PER;
+    constexpr int PAD = PER + 1;             // LDS row of a lane: PER values + 1 (fewer bank conflicts)
+    __shared__ uint64_t s_x[16][64 * PAD];   // per wave: its block, lane-major
+    __shared__ uint64_t s_w[16];
+    __shared__ uint64_t s_carry;
+    uint64_t* const arr = blockIdx.x ? v2 : v;
     const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
-    if (t < NA) s_carry[t] = 0;
+    if (t == 0) s_carry = 0;
     __syncthreads();
     for (uint64_t base = 0; base < ntiles; base += 16 * BLK) {
         const uint64_t wb = base + (uint64_t)wid * BLK;
-        uint64_t sum[NA], inc[NA];
 #pragma unroll
-        for (int a = 0; a < NA; ++a) {
-            const uint64_t* arr = a ? v2 : v;
-#pragma unroll
-            for (int k = 0; k < PER; ++k) {   // value j = 64 k + lane of the block -> row j / PER, column j % PER
-                const int j = 64 * k + lane;
-                const uint64_t i = wb + (uint64_t)j;
-                s_x[a][wid][(j / PER) * PAD + j % PER] = i < ntiles ? arr[i] : 0;
-            }
+        for (int k = 0; k < PER; ++k) {   // value j = 64 k + lane of the block -> row j / PER, column j % PER
+            const int j = 64 * k + lane;
+            const uint64_t i = wb + (uint64_t)j;
+            s_x[wid][(j / PER) * PAD + j % PER] = i < ntiles ? arr[i] : 0;
         }
         hy_wave_sync();
+        uint64_t* row = &s_x[wid][lane * PAD];
+        uint64_t run = 0;
 #pragma unroll
-        for (int a = 0; a < NA; ++a) {
-            uint64_t* row = &s_x[a][wid][lane * PAD];
-            uint64_t run = 0;
-#pragma unroll
-            for (int k = 0; k < PER; ++k) {   // exclusive within the lane's row
-                const uint64_t x = row[k];
-                row[k] = run;
-                run += x;
-            }
-            sum[a] = run;
-            inc[a] = wave_incl_scan(run, lane);
-            if (lane == 63) s_w[a][wid] = inc[a];
+        for (int k = 0; k < PER; ++k) {   // exclusive within the lane's row
+            const uint64_t x = row[k];
+            row[k] = run;
+            run += x;
         }
+        const uint64_t inc = wave_incl_scan(run, lane);
+        if (lane == 63) s_w[wid] = inc;
         __syncthreads();
+        uint64_t wpre = 0;
+        for (int w = 0; w < wid; ++w) wpre += s_w[w];
+        const uint64_t off = s_carry + wpre + inc - run;   // before this lane's row
 #pragma unroll
-        for (int a = 0; a < NA; ++a) {
-            uint64_t wpre = 0;
-            for (int w = 0; w < wid; ++w) wpre += s_w[a][w];
-            const uint64_t off = s_carry[a] + wpre + inc[a] - sum[a];   // before this lane's row
-            uint64_t* row = &s_x[a][wid][lane * PAD];
-#pragma unroll
-            for (int k = 0; k < PER; ++k) row[k] += off;
-        }
+        for (int k = 0; k < PER; ++k) row[k] += off;
         hy_wave_sync();
 #pragma unroll
-        for (int a = 0; a < NA; ++a) {
-            uint64_t* arr = a ? v2 : v;
-#pragma unroll
-            for (int k = 0; k < PER; ++k) {
-                const int j = 64 * k + lane;
-                const uint64_t i = wb + (uint64_t)j;
-                if (i < ntiles) arr[i] = s_x[a][wid][(j / PER) * PAD + j % PER];
-            }
+        for (int k = 0; k < PER; ++k) {
+            const int j = 64 * k + lane;
+            const uint64_t i = wb + (uint64_t)j;
+            if (i < ntiles) arr[i] = s_x[wid][(j / PER) * PAD + j % PER];
         }
         __syncthreads();
-        if (t < NA) {
+        if (t == 0) {
             uint64_t tot = 0;
-            for (int w = 0; w < 16; ++w) tot += s_w[t][w];
-            s_carry[t] += tot;
+            for (int w = 0; w < 16; ++w) tot += s_w[w];
+            s_carry += tot;
         }
         __syncthreads();
     }
-    if (t == 0) {
-        v[ntiles] = s_carry[0];
-        if (TWO) v2[ntiles] = s_carry[NA - 1];
-    }
+    if (t == 0) arr[ntiles] = s_carry;
 }
 
 // keys only (hyobfs_salamander_key): key[i] = BLAKE2b-256(PSK || salts[i])
@@ -331,10 +311,8 @@ hipError_t launch_salamander(bool obf, const BatchParams& b, const KeyParams& k,
             hipLaunchKernelGGL(tile_sums_kernel<true>, grid, block, 0, s, bp, ntiles);
         else
             hipLaunchKernelGGL(tile_sums_kernel<false>, grid, block, 0, s, bp, ntiles);
-        if (bp.in_tile_sums)
-            hipLaunchKernelGGL(scan_tiles_kernel<true>, dim3(1), dim3(1024), 0, s, bp.tile_sums, bp.in_tile_sums, ntiles);
-        else
-            hipLaunchKernelGGL(scan_tiles_kernel<false>, dim3(1), dim3(1024), 0, s, bp.tile_sums, bp.in_tile_sums, ntiles);
+        hipLaunchKernelGGL(scan_tiles_kernel, dim3(bp.in_tile_sums ? 2 : 1), dim3(1024), 0, s, bp.tile_sums,
+                           bp.in_tile_sums, ntiles);
         bp.tile_prefix = bp.tile_sums;
         bp.in_tile_prefix = bp.in_tile_sums;
         if (obf)

@@ -39,6 +39,7 @@ else:
     out_len = torch.empty(P, dtype=torch.int32, device=dev)
     back = torch.empty(total_in + 16, dtype=torch.uint8, device=dev)
     nws = max(o.workspace_bytes(inp=inp, n=P, in_off=in_off, in_len=lens, out=wire, out_cap=cap),
+              o.workspace_bytes(inp=inp, n=P, in_len=lens, out=wire, out_cap=cap),   # bimodal_alt: both layouts
               o.workspace_bytes(inp=wire, n=P, in_off=None if in_off is None else out_off, in_len=out_len, out=back, out_cap=total_in))
     ws = torch.empty(max(nws, 16), dtype=torch.uint8, device=dev)
     if wl == "bimodal_alt":   # 20 warm-up launches, then contiguous and explicit offsets alternating
@@ -49,7 +50,7 @@ else:
     for _ in range(K):
         o.obfuscate_batch(inp, P, in_off=in_off, in_len=lens, salts=salts, out=wire, out_cap=cap,
                           out_off=out_off, out_len=out_len, workspace=ws, workspace_bytes=ws.numel())
-    for _ in range(K if os.environ.get("PROF_ORDER") != "deobf_last_obf" else 0):
+    for _ in range(K):
         o.deobfuscate_batch(wire, P, in_off=None if in_off is None else out_off, in_len=out_len, out=back, out_cap=total_in,
                             workspace=ws, workspace_bytes=ws.numel())
 torch.cuda.synchronize()
