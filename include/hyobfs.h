@@ -161,8 +161,9 @@ size_t hyobfs_salamander_deobfuscate(hyobfs_salamander* ctx, const uint8_t* in,
  *   input   : len  L_i = in_len ? in_len[i] : len_uniform
  *             bytes at in + (in_off ? in_off[i] : i * in_stride)       (any alignment)
  *             CONTIGUOUS input: in_off == NULL, in_stride == 0 and in_len != NULL
- *             put datagram i at in + L_0 + ... + L_{i-1} (back to back; a
- *             16-byte aligned `in` lets packed output run the stream kernel)
+ *             put datagram i at in + L_0 + ... + L_{i-1} (back to back; no
+ *             offset array; with HYOBFS_KERNEL_STREAM and a 16-byte aligned
+ *             `in`, packed output runs the stream kernel)
  *   salt    : obfuscate only: salts[i], 8 bytes, little-endian u64
  *             (salt byte b = (salts[i] >> 8b) & 0xff)
  *   output  : W_i = L_i + 8 (obfuscate) or L_i - 8 (deobfuscate)

@@ -8,10 +8,11 @@ streaming kernel by up to +-5 % between processes, is shared.
 
 A name ending in "!" is an ablation build (wrong output): its wire is not checked.
 AB_WORKLOAD=bimodal runs BASELINE configs[2] instead (P datagrams of the 40 % 64 B /
-60 % 1350 B mix, default 4M, packed output).  Bimodal input is contiguous (in_off NULL:
-the stream kernel under auto); a kernel name with "@off" passes explicit in_off /
-out_off arrays instead (the round-3 layout: the wave kernel).  AB_LEN_MAP="1350:1344"
-replaces lengths (alignment studies).
+60 % 1350 B mix, default 4M, packed output).  Bimodal input is contiguous (in_off NULL,
+as bench.py); a kernel name with "@off" passes explicit in_off / out_off arrays instead.
+AB_LEN_MAP="1350:1344" replaces lengths (alignment studies).  The first variant of a run
+measures ~1.5 % slow (profiles/r04_ab_wave_wu_order_control.txt): put a throw-away
+copy of a build first when differences of that size matter.
 """
 import os
 import statistics
