@@ -99,6 +99,9 @@ def test_header_abi_version_matches_bindings():
     text = open(os.path.join(ROOT, "include", "hyobfs.h")).read()
     assert int(re.search(r"#define HYOBFS_ABI_VERSION (\d+)", text).group(1)) == _lib.ABI_VERSION
     assert int(re.search(r"#define HYOBFS_ERR_CLOSED \((-\d+)\)", text).group(1)) == _lib.HYOBFS_ERR_CLOSED
+    from hysteria_amd.salamander import SalamanderObfuscator
+    kernels = {m.group(1).lower(): int(m.group(2)) for m in re.finditer(r"HYOBFS_KERNEL_(\w+) = (\d+)", text)}
+    assert kernels == SalamanderObfuscator.KERNELS   # auto, wave, tile, stream
 
 
 def test_load_refuses_other_abi_version(tmp_path):

@@ -96,6 +96,19 @@ def test_edge_rules_per_packet(obfs):
     assert obfs.deobfuscate(b"\x00" * 20, bytearray(12)) == 12
 
 
+def test_set_kernel_accepts_the_header_values_only(gpu):
+    """hyobfs_salamander_set_kernel: HYOBFS_KERNEL_AUTO..STREAM accepted, anything else
+    HYOBFS_ERR_INVALID (include/hyobfs.h)."""
+    import hysteria_amd
+    from hysteria_amd import _lib
+    with hysteria_amd.SalamanderObfuscator(PSK, 0) as o:
+        lib = _lib.load()
+        for k in range(4):
+            assert lib.hyobfs_salamander_set_kernel(o._h, k) == 0
+        for k in (-1, 4, 99):
+            assert lib.hyobfs_salamander_set_kernel(o._h, k) == _lib.HYOBFS_ERR_INVALID
+
+
 def test_reference_roundtrip_1000x1200_auto_salts(obfs):
     """TestSalamanderObfuscator (salamander_test.go:32-45) on the GPU path."""
     rng = np.random.default_rng(3)
