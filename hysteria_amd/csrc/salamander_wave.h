@@ -32,8 +32,8 @@ namespace hyobfs {
 constexpr int kGroup = 64;           // datagrams per wave group (= lanes)
 constexpr int kWavesPerBlock = 4;    // independent waves per workgroup
 #ifndef HY_WU
-#define HY_WU 8
-#endif
+#define HY_WU 6                      // 8 spills 12 B with the store order below; 4, 6, 8 run alike
+#endif                               // (profiles/r04_ab_wave_store_waits.txt)
 constexpr int kWU = HY_WU;           // chunks per lane per sweep iteration
 #ifndef HY_RUN_LOG2
 #define HY_RUN_LOG2 3
@@ -469,15 +469,32 @@ salamander_wave_kernel(BatchParams B, KeyParams K) {
             }
         }
     };
-    auto retire = [&](uint32_t c0, const Sweep& R) {
+    // Every chunk's value is finished before the first store: the stores then leave
+    // from distinct registers.  (Computing each value into the registers the
+    // previous store read made the compiler wait for that store to complete,
+    // vmcnt(0), before every store of the iteration.)
+    auto retire = [&](uint32_t c0, Sweep& R) {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            if (!R.fast[u]) continue;
             const uint32_t a = (c0 + u * kGroup + lane) << 4;
             const uint4 kk = G.key[2 * R.q[u] + ((a >> 4) & 1)];
             u128 k128;
             __builtin_memcpy(&k128, &kk, 16);
-            store16_stream(B.out + (G.delta[R.q[u]] + a), R.v[u] ^ k128);
+            R.v[u] ^= k128;
+#ifndef HYOBFS_EMULATE
+            // keep each value in its own registers (no instruction): otherwise the
+            // compiler sinks the XOR into the conditional store below, into the
+            // registers the previous store read
+            uint64_t lo = (uint64_t)R.v[u], hi = (uint64_t)(R.v[u] >> 64);
+            __asm__ volatile("" : "+v"(lo), "+v"(hi));
+            R.v[u] = (u128)hi << 64 | lo;
+#endif
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (!R.fast[u]) continue;
+            const uint32_t a = (c0 + u * kGroup + lane) << 4;
+            store16_stream(B.out + (G.delta[R.q[u]] + a), R.v[u]);
         }
     };
     constexpr uint32_t STEP = kGroup * U;
