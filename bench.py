@@ -47,12 +47,10 @@ BIMODAL_MIN_WARMUP = 20
 KERNEL_NAMES = {
     "uniform": {"auto": "salamander_tile_kernel<obfuscate> (salamander_tile.h)",
                 "tile": "salamander_tile_kernel<obfuscate> (salamander_tile.h)",
-                "wave": "salamander_wave_kernel<obfuscate, slotted> (salamander_wave.h)",
-                "stream": "salamander_tile_kernel<obfuscate> (salamander_tile.h)"},
+                "wave": "salamander_wave_kernel<obfuscate, slotted> (salamander_wave.h)"},
     "bimodal": {"auto": "salamander_wave_kernel<obfuscate, packed> (salamander_wave.h) + width/length scan (2 launches)",
                 "tile": "salamander_wave_kernel<obfuscate, packed> (salamander_wave.h) + width/length scan (2 launches)",
-                "wave": "salamander_wave_kernel<obfuscate, packed> (salamander_wave.h) + width/length scan (2 launches)",
-                "stream": "salamander_stream_kernel<obfuscate> (salamander_stream.h) + 3 prepass launches"},
+                "wave": "salamander_wave_kernel<obfuscate, packed> (salamander_wave.h) + width/length scan (2 launches)"},
 }
 
 
@@ -68,7 +66,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--no-bimodal", action="store_true", help="N=1: skip the configs[2] sub-object")
-    ap.add_argument("--kernel", choices=["auto", "wave", "tile", "stream"], default="auto")
+    ap.add_argument("--kernel", choices=["auto", "wave", "tile"], default="auto")
     return ap.parse_args()
 
 
@@ -247,7 +245,7 @@ def main():
     import torch
     import torch.distributed as dist
     import hysteria_amd as hy
-    from hysteria_amd.shard import weak_shard
+    from hysteria_amd.shard import check_rank_devices, weak_shard
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -277,6 +275,15 @@ def main():
         dist.all_gather(out, torch.tensor([x], dtype=torch.float64))
         return [float(t[0]) for t in out]
 
+    # which card each rank bound: rank setup fails if two ranks share one while the
+    # node has a card per rank (hysteria_amd/shard.py check_rank_devices)
+    bus_id = hy.device_pci_bus_id(local)
+    if world > 1:
+        bus_ids = [None] * world
+        dist.all_gather_object(bus_ids, bus_id)
+    else:
+        bus_ids = [bus_id]
+    shared = check_rank_devices(bus_ids, torch.cuda.device_count())
     obfs = hy.SalamanderObfuscator(PSK, local)
     obfs.set_kernel(args.kernel)
     stream = torch.cuda.current_stream(dev)
@@ -323,8 +330,9 @@ def main():
             deob["traffic"] = t["hbm_bytes_per_launch"]
             deob["traffic_over_algorithmic"] = round(t["hbm_bytes_per_launch"] / w["deobf_bytes"], 4)
         per_gpu = [round(w["payload"] * args.steps / x / 2**30, 2) for x in allgather(mine_obf)]
+        launch_ms = [round(x * 1e3, 4) for x in allgather(ev_obf)]
         return dict(value=total_payload / wall_obf / 2**30, ms=wall_obf / args.steps * 1e3, roofline=roof,
-                    deobfuscate=deob, per_gpu=per_gpu)
+                    deobfuscate=deob, per_gpu=per_gpu, launch_ms=launch_ms)
 
     if args.workload == "uniform":
         P = args.packets_per_gpu or ((1 << 20) if world == 1 else (1 << 23))
@@ -370,6 +378,8 @@ def main():
         "config": config,
         "roofline": m["roofline"],
         "per_gpu_GiBs": m["per_gpu"],
+        "ranks": [{"rank": r, "pci_bus_id": bus_ids[r], "obf_call_ms": m["launch_ms"][r]} for r in range(world)],
+        "devices_shared": shared,
         "deobfuscate": m["deobfuscate"],
         "parity": parity,
     }

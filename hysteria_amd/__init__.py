@@ -16,6 +16,7 @@ from .salamander import (  # noqa: F401
     build_id,
     deobfuscate_batch_sharded,
     device_count,
+    device_pci_bus_id,
     new_salamander_obfuscator,
     obfuscate_batch_sharded,
     synth_bimodal_lengths,
@@ -26,7 +27,7 @@ from .salamander import (  # noqa: F401
 
 __all__ = [
     "SM_KEY_LEN", "SM_PSK_MIN_LEN", "SM_SALT_LEN", "UDP_BUFFER_SIZE", "PSKTooShortError",
-    "SalamanderObfuscator", "device_count", "new_salamander_obfuscator", "synth_bimodal_lengths",
+    "SalamanderObfuscator", "device_count", "device_pci_bus_id", "new_salamander_obfuscator", "synth_bimodal_lengths",
     "synth_stream", "synth_u64", "workspace_size", "SalamanderPacketConn", "wrap_packet_conn_salamander",
     "obfuscate_batch_sharded", "deobfuscate_batch_sharded", "gecko", "GeckoOptions", "GeckoPacketConn",
     "wrap_packet_conn_gecko", "build_id",

@@ -21,7 +21,7 @@ HYOBFS_ERR_NOMEM = -4
 HYOBFS_ERR_NO_DEVICE = -5
 HYOBFS_ERR_IO = -6
 HYOBFS_ERR_CLOSED = -7
-ABI_VERSION = 2   # the HYOBFS_ABI_VERSION these bindings are written for (include/hyobfs.h)
+ABI_VERSION = 3   # the HYOBFS_ABI_VERSION these bindings are written for (include/hyobfs.h)
 
 
 class HyobfsBatch(ctypes.Structure):
@@ -97,6 +97,7 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         "hyobfs_build_id": (ctypes.c_char_p, []),
         "hyobfs_status_string": (ctypes.c_char_p, [i32]),
         "hyobfs_device_count": (i32, []),
+        "hyobfs_device_pci_bus_id": (i32, [i32, ctypes.c_char_p, i32]),
         "hyobfs_salamander_new": (i32, [vp, sz, i32, ctypes.POINTER(ctypes.c_void_p)]),
         "hyobfs_salamander_free": (None, [pctx]),
         "hyobfs_salamander_device": (i32, [pctx]),

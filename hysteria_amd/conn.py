@@ -33,6 +33,7 @@ import errno
 import os
 import socket
 import struct
+import threading
 
 from . import _lib
 from ._lib import HyobfsDgram, check
@@ -106,6 +107,7 @@ class SalamanderPacketConn:
             self.settimeout(self._timeout)
         h = ctypes.c_void_p()
         self._closed = False
+        self._close_lock = threading.Lock()
         check(self._lib.hyobfs_conn_wrap(sock.fileno(), obfuscator._h, batch, ctypes.byref(h)), "hyobfs_conn_wrap")
         self._h = h
         self.batch = batch
@@ -117,11 +119,12 @@ class SalamanderPacketConn:
         after close raise OSError(EBADF) (Go: net.ErrClosed); the handle is freed
         only when this object goes away (hyobfs_conn_free), so threads still
         inside a call never touch freed memory.  A second close raises too."""
-        if self._closed:
-            raise OSError(errno.EBADF, "close: use of closed connection")
-        self._closed = True
-        self._sock.detach()            # the C side owns and closes the fd
-        check(self._lib.hyobfs_conn_close(self._h), "hyobfs_conn_close")
+        with self._close_lock:         # one closer detaches the socket; the others get EBADF
+            if self._closed:
+                raise OSError(errno.EBADF, "close: use of closed connection")
+            self._closed = True
+            self._sock.detach()        # the C side owns and closes the fd
+        _check_conn(self._lib.hyobfs_conn_close(self._h), "close")
 
     def __enter__(self):
         return self

@@ -21,7 +21,6 @@
 #include "kernels.h"
 #include "salamander_device.h"
 #include "salamander_wave.h"   // wave_key<SW>: the key unrolled per salt word
-#include "salamander_tile.h"   // quad_key<SW>: four lanes per key (the wire-tile kernel)
 #include "../../include/hyobfs_gecko.h"
 
 namespace hyobfs {
@@ -354,15 +353,13 @@ __device__ __forceinline__ void gecko_encode_aligned(const KeyParams& K, const h
 #define HY_GK_ATTR __attribute__((amdgpu_waves_per_eu(HY_GK_WPE)))
 #endif
 template <int SW>
-__global__ __launch_bounds__(256) HY_GK_ATTR void gecko_encode_kernel(KeyParams K, hyobfs_gecko_batch B,
-                                                                    const uint32_t* tiled) {
+__global__ __launch_bounds__(256) HY_GK_ATTR void gecko_encode_kernel(KeyParams K, hyobfs_gecko_batch B) {
     __shared__ GeckoGroup gg[4];
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     GeckoGroup& G = gg[wid];
     const uint64_t f0 = ((uint64_t)blockIdx.x * 4 + wid) * 64;
     if (f0 >= B.n) return;
-    if (tiled && *tiled == 0) return;   // the wire-tile kernel took this batch (gecko_tile_kernel)
     // ---- 1. lane l: frame f0 + l's record, offsets, salt and key into LDS
     const uint64_t f = f0 + lane;
     uint32_t nwin = 0, plain = 0;
@@ -530,230 +527,6 @@ __global__ __launch_bounds__(256) HY_GK_ATTR void gecko_encode_kernel(KeyParams 
     edges(emask);   // ---- 3. all edge windows after the sweep
 }
 
-// ------------------------------------------------------------ wire tiles
-// When the caller gives out_cap and every frame is valid and lies after the one
-// before it (back to back or with gaps: what writeFragmented and plan_fragments
-// produce), the wire is cut into tiles of kGT bytes, 128-byte aligned, and
-// one workgroup per tile: wave 0 loads the records of the frames that
-// touch the tile, all four waves hash their keys (four lanes per key, quad_key of
-// salamander_tile.h) and rotate them to the wire phase, the chunks holding a frame's
-// salt, header, padding/chunk seam or end are assembled once (gk_contrib) and parked,
-// and all 256 threads sweep the tile's 16-byte chunks: padding from the ChaCha8
-// keystream (a quad per 64-byte block), message bytes by one unaligned load, each
-// leaving as one aligned streaming store; a line is written whole by one workgroup.
-// gecko_tiles_kernel maps tiles to their first frame and decides: any other
-// placement leaves the batch to the wave-group kernel above (which checks the flag).
-constexpr uint64_t kGT = 16384;     // wire bytes per tile
-constexpr uint64_t kGTBack = 4096;  // a tile's first frame starts < 2048 B before it: the group base
-                                    // tT - 4096 keeps every rs >= 0 (64-byte aligned for the keystream)
-constexpr int kGC = 5;              // boundary candidates per frame
-
-struct GkTiles {
-    uint32_t* first;           // ntiles_max: first frame whose wire ends after the tile's start
-    unsigned long long* end;   // wire end of the last frame
-    uint32_t* unordered;       // 1: some frame is invalid, past out_cap or before its predecessor's end
-    uint64_t ntiles_max;
-};
-
-__device__ __forceinline__ bool gk_frame(const hyobfs_gecko_batch& B, uint64_t f, uint64_t& start, uint32_t& hp,
-                                         uint32_t& plain) {
-    const hyobfs_gecko_frame fr = B.frames[f];
-    const uint32_t total = fr.idx_total & 0x0f, idx = fr.idx_total >> 4;
-    hp = HYOBFS_GECKO_HEADER_LEN + fr.pad_len;
-    const uint64_t plain64 = (uint64_t)hp + fr.chunk_len;
-    plain = (uint32_t)plain64;
-    start = B.out_off[f];
-    return total >= HYOBFS_GECKO_MIN_CHUNKS && total <= HYOBFS_GECKO_MAX_CHUNKS && idx < total &&
-           HYOBFS_SALT_LEN + plain64 <= HYOBFS_GECKO_BUFFER_SIZE;
-}
-
-// Thread per frame: checks the order, writes first[t] for the tiles whose start
-// lies in (end of frame f - 1, end of frame f].
-__global__ __launch_bounds__(256) void gecko_tiles_kernel(hyobfs_gecko_batch B, GkTiles S) {
-    const uint64_t f = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-    if (f >= B.n) return;
-    uint64_t st, pst = 0;
-    uint32_t hp, pl, php, ppl;
-    const bool ok = gk_frame(B, f, st, hp, pl);
-    const uint64_t end = st + HYOBFS_SALT_LEN + pl;
-    uint64_t prev_end = 0;
-    bool pok = true;
-    if (f > 0) {
-        pok = gk_frame(B, f - 1, pst, php, ppl);
-        prev_end = pst + HYOBFS_SALT_LEN + ppl;
-    }
-    if (!ok || !pok || end > B.out_cap || st < prev_end || (f > 0 && pst > st)) {
-        *S.unordered = 1;
-        return;
-    }
-    for (uint64_t t = (prev_end + kGT - 1) / kGT; t * kGT < end && t < S.ntiles_max; ++t) S.first[t] = (uint32_t)f;
-    if (f + 1 == B.n) *S.end = end;
-}
-
-template <int SW>
-__global__ __launch_bounds__(256) HY_GK_ATTR void gecko_tile_kernel(KeyParams K, hyobfs_gecko_batch B, GkTiles S,
-                                                                    uint64_t t0) {
-    __shared__ GeckoGroup G;
-    __shared__ gk_u128 s_park[kGC * 64];
-    __shared__ uint8_t s_parked[kGC * 64];
-    const uint32_t tid = threadIdx.x, lane = tid & 63;
-    const uint32_t wid = uni32(tid >> 6);
-    if (uni32(*S.unordered)) return;   // the wave-group kernel runs this batch
-    const uint64_t E = uni64(*S.end);
-    const uint64_t ntiles = (E + kGT - 1) / kGT;
-    const GkPad P = gk_pad_params(B);
-    // one workgroup per wire tile (a persistent loop over tiles made every tile wait
-    // for the previous one's stores: 1.35 ms against 0.57 for the wave-group kernel)
-    const uint64_t t = t0 + blockIdx.x;
-    if (t < ntiles) {
-        const uint64_t tT = t * kGT;
-        const uint64_t base = tT >= kGTBack ? tT - kGTBack : 0;
-        const uint32_t xo = (uint32_t)(tT - base);                          // the tile's start, group-relative
-        const uint32_t xe = xo + (uint32_t)min<uint64_t>(kGT, E - tT);     // its end
-        uint64_t g0 = uni32(S.first[t]);
-        uint32_t prev_end = 0;   // end of the previous pass's last frame (group-relative)
-        for (;;) {
-            // ---- wave 0: the pass's frames (those starting before the tile's end) into LDS
-            if (wid == 0) {
-                const uint64_t f = g0 + lane;
-                uint64_t st = 0;
-                uint32_t hp = 0, pl = 0;
-                bool live = f < B.n;
-                if (live) {
-                    (void)gk_frame(B, f, st, hp, pl);   // valid: the prepass checked every frame
-                    live = st < base + xe;
-                }
-                uint64_t salt = 0;
-                if (live) {
-                    const hyobfs_gecko_frame fr = B.frames[f];
-                    G.chunk_off[lane] = fr.chunk_off;
-                    G.hdr[lane] = (uint64_t)HYOBFS_GECKO_FLAG_FRAGMENT | (uint64_t)fr.msg_id << 8 |
-                                  (uint64_t)fr.idx_total << 16 | (uint64_t)(fr.pad_len >> 8) << 24 |
-                                  (uint64_t)(fr.pad_len & 0xff) << 32;
-                    salt = B.salts[f];
-                }
-                G.rs[lane] = live ? (uint32_t)(st - base) : 0xFFFFFFFFu;
-                if (lane == 0) G.rs[64] = 0xFFFFFFFFu;
-                G.hp_plain[lane] = live ? hp | pl << 16 : 0u;
-                G.salt[lane] = salt;
-            }
-            hy_lds_barrier();
-            const uint32_t mp = uni32((uint32_t)__builtin_popcountll(__ballot(G.rs[lane] != 0xFFFFFFFFu)));
-            // ---- keys: wave w hashes frames 16w .. 16w + 15, four lanes each, rotated so
-            // that group-relative wire address a indexes byte a mod 32
-            if (16u * wid < mp) {
-                const uint32_t k = 16u * wid + (lane >> 2), qi = lane & 3u;
-                const uint32_t kk = k < mp ? k : 0u;
-                const uint64_t kw = quad_key<SW>(K, G.salt[kk], qi);
-                const uint32_t r = (G.rs[kk] + HYOBFS_SALT_LEN) & 31u;
-                const uint32_t st8 = (8u * qi - r) & 31u, w0 = st8 >> 3, sh = (st8 & 7u) * 8u;
-                const uint64_t a = __shfl(kw, (int)((lane & ~3u) | w0), 64);
-                const uint64_t b = __shfl(kw, (int)((lane & ~3u) | ((w0 + 1) & 3u)), 64);
-                if (k < mp) reinterpret_cast<uint64_t*>(G.key)[4 * k + qi] = sh ? (a >> sh) | (b << (64 - sh)) : a;
-            }
-            __syncthreads();
-            const uint32_t pass_end = mp ? G.rs[mp - 1] + HYOBFS_SALT_LEN + (G.hp_plain[mp - 1] >> 16) : xo;
-            // ---- boundary chunks: candidate c of frame k (wave w: candidates w and, for
-            // wave 0, 4), parked when complete and frame k is the first one touching it
-            auto cand = [&](uint32_t k, int c) -> uint32_t {
-                const uint32_t rs = G.rs[k], hpl = G.hp_plain[k], hp = hpl & 0xffff, pl = hpl >> 16;
-                const uint32_t seam = rs + HYOBFS_SALT_LEN + hp;
-                return c == 0 ? rs >> 4 : c == 1 ? (rs + HYOBFS_SALT_LEN + HYOBFS_GECKO_HEADER_LEN - 1) >> 4
-                     : c == 2 ? (seam - 1) >> 4 : c == 3 ? seam >> 4 : (rs + HYOBFS_SALT_LEN + pl - 1) >> 4;
-            };
-            for (int c = (int)wid; c < kGC; c += 4) {
-                if (lane >= mp) continue;
-                const uint32_t k = lane;
-                uint8_t pk = 0;
-                const uint32_t ch = cand(k, c), a = 16u * ch;
-                bool dup = false;
-                for (int u = 0; u < c; ++u) dup = dup || cand(k, u) == ch;
-                int32_t p, php;
-                auto interior = [&](uint32_t q, uint32_t aa) {
-                    const uint32_t hpl = G.hp_plain[q];
-                    php = (int32_t)(hpl & 0xffff);
-                    const int32_t pl = (int32_t)(hpl >> 16);
-                    p = (int32_t)aa - (int32_t)G.rs[q] - HYOBFS_SALT_LEN;
-                    return hpl != 0 && ((p >= (int32_t)HYOBFS_GECKO_HEADER_LEN && p + 16 <= php) || (p >= php && p + 16 <= pl));
-                };
-                const uint32_t pe = k ? G.rs[k - 1] + HYOBFS_SALT_LEN + (G.hp_plain[k - 1] >> 16) : prev_end;
-                const bool touches = G.rs[k] < a + 16 && G.rs[k] + HYOBFS_SALT_LEN + (G.hp_plain[k] >> 16) > a;
-                if (!dup && touches && a >= xo && a < xe && !interior(k, a) && (pe <= a || k == 0)) {
-                    gk_u128 rr = 0;
-                    uint32_t cov = 0;
-                    for (uint32_t q = k; q < mp && G.rs[q] < a + 16; ++q) gk_contrib(B, P, G, base, q, a, rr, cov);
-                    if (cov == 0xFFFFu && (k > 0 || prev_end <= a)) {
-                        s_park[kGC * k + c] = rr;
-                        pk = 1;
-                    } else if (cov) {
-                        store_masked(B.out + base + a, rr, cov);   // gaps, pass edges, the wire's end
-                    }
-                }
-                s_parked[kGC * k + c] = pk;
-            }
-            hy_lds_barrier();
-            // ---- sweep: the chunks of [max(xo, start of the pass), min(xe, pass end))
-            const uint32_t lo = g0 == uni32(S.first[t]) ? xo : max(xo, G.rs[0] & ~15u);
-            const uint32_t hi = min(xe, (pass_end + 15) & ~15u);
-            for (uint32_t a0 = lo; a0 < hi; a0 += 16u * 256u * (uint32_t)kGkU) {
-                gk_u128 v[kGkU];
-                uint8_t kind[kGkU];   // 0 nothing, 1 padding, 2 message, 3 parked
-                uint32_t kq[kGkU];
-#pragma unroll
-                for (int u = 0; u < kGkU; ++u) {
-                    const uint32_t a = a0 + 16u * (tid + 256u * (uint32_t)u);
-                    kind[u] = 0;
-                    kq[u] = 0;
-                    v[u] = 0;
-                    const uint8_t* src = hy_safe_line();
-                    if (a < hi) {
-                        uint32_t q = 0;
-#pragma unroll
-                        for (uint32_t step = 32; step; step >>= 1) q = G.rs[q + step] <= a ? q + step : q;
-                        kq[u] = q;
-                        const uint32_t hpl = G.hp_plain[q];
-                        const int32_t hp = (int32_t)(hpl & 0xffff), pl = (int32_t)(hpl >> 16);
-                        const int32_t p = (int32_t)a - (int32_t)G.rs[q] - HYOBFS_SALT_LEN;
-                        if (hpl && p >= (int32_t)HYOBFS_GECKO_HEADER_LEN && p + 16 <= hp) {
-                            kind[u] = 1;
-                        } else if (hpl && p >= hp && p + 16 <= pl) {
-                            kind[u] = 2;
-                            src = B.msg + G.chunk_off[q] + (p - hp);
-                        } else {   // a parked chunk: its owner is the first frame touching it
-                            uint32_t own = q;
-                            if (!(hpl && G.rs[q] + HYOBFS_SALT_LEN + (uint32_t)pl > a)) own = q + 1;
-                            if (own < mp) {
-#pragma unroll
-                                for (int c = 0; c < kGC; ++c) {
-                                    if (kind[u] == 0 && cand(own, c) == (a >> 4) && s_parked[kGC * own + c]) {
-                                        kind[u] = 3;
-                                        v[u] = s_park[kGC * own + c];
-                                    }
-                                }
-                            }
-                        }
-                    }
-                    if (kind[u] != 3) v[u] = gk_load16u(src);   // unconditional: exact vmcnt waits
-                }
-#pragma unroll
-                for (int u = 0; u < kGkU; ++u) {
-                    const uint32_t a = a0 + 16u * (tid + 256u * (uint32_t)u);
-                    if (__ballot(kind[u] == 1)) {   // the whole wave: a quad computes one 64-byte block
-                        const gk_u128 ks = gk_ks_quad(P, (base + a) >> 6, lane & 3u);
-                        if (kind[u] == 1) v[u] = ks;
-                    }
-                    if (kind[u] == 1 || kind[u] == 2) v[u] ^= G.key[2 * kq[u] + ((a >> 4) & 1)];
-                    if (kind[u]) store16_stream(B.out + base + a, v[u]);
-                }
-            }
-            prev_end = pass_end;
-            hy_lds_barrier();
-            if (mp < 64 || g0 + 64 >= B.n) break;
-            g0 += 64;
-        }
-    }
-}
-
 __global__ __launch_bounds__(256) void gecko_parse_kernel(const uint8_t* in, const uint64_t* in_off,
                                                           const uint32_t* in_len, uint64_t n,
                                                           hyobfs_gecko_parsed* out) {
@@ -788,48 +561,14 @@ __global__ __launch_bounds__(256) void gecko_parse_kernel(const uint8_t* in, con
     out[i] = r;
 }
 
-uint64_t gecko_tiles_workspace_bytes(uint64_t out_cap) {
-    return out_cap ? 16 + 4 * ((out_cap + kGT - 1) / kGT) : 0;
-}
-
-template <int SW>
-static void launch_gecko_tile_sw(const KeyParams& k, const hyobfs_gecko_batch& b, const GkTiles& S, hipStream_t s) {
-    // one workgroup per tile out_cap allows (those past the wire's end exit at once),
-    // launches of at most 65536 tiles (1 GiB of wire)
-    constexpr uint64_t kLaunch = 65536;
-    const uint64_t nt = S.ntiles_max < 1 ? 1 : S.ntiles_max;
-    for (uint64_t t0 = 0; t0 < nt; t0 += kLaunch) {
-        const uint64_t g = nt - t0 < kLaunch ? nt - t0 : kLaunch;
-        hipLaunchKernelGGL(gecko_tile_kernel<SW>, dim3((uint32_t)g), dim3(256), 0, s, k, b, S, t0);
-    }
-}
-
-hipError_t launch_gecko_encode(const KeyParams& k, const hyobfs_gecko_batch& b, void* ws, hipStream_t s) {
+hipError_t launch_gecko_encode(const KeyParams& k, const hyobfs_gecko_batch& b, hipStream_t s) {
     if (b.n == 0) return hipSuccess;
     // instantiated per salt word (salamander_inst.hip's rule): the PSK's message words
     // stay scalar, only the salt's one or two words are per lane
     const dim3 grid((uint32_t)((b.n + 255) / 256)), block(256);
-    const uint32_t* tiled = nullptr;
-    if (b.out_cap && ws) {   // the wire-tile path; the wave-group kernel runs if it declines
-        GkTiles S;
-        S.end = static_cast<unsigned long long*>(ws);
-        S.unordered = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(ws) + 8);
-        S.first = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(ws) + 16);
-        S.ntiles_max = (b.out_cap + kGT - 1) / kGT;
-        if (hipMemsetAsync(ws, 0, 16, s) != hipSuccess) return hipErrorInvalidValue;
-        hipLaunchKernelGGL(gecko_tiles_kernel, grid, block, 0, s, b, S);
-        switch (k.salt_pos >> 3) {
-#define HY_CASE(n) \
-    case n: launch_gecko_tile_sw<n>(k, b, S, s); break;
-            HY_CASE(0) HY_CASE(1) HY_CASE(2) HY_CASE(3) HY_CASE(4) HY_CASE(5) HY_CASE(6) HY_CASE(7)
-            HY_CASE(8) HY_CASE(9) HY_CASE(10) HY_CASE(11) HY_CASE(12) HY_CASE(13) HY_CASE(14) HY_CASE(15)
-#undef HY_CASE
-        }
-        tiled = S.unordered;
-    }
     switch (k.salt_pos >> 3) {
 #define HY_CASE(n) \
-    case n: hipLaunchKernelGGL(gecko_encode_kernel<n>, grid, block, 0, s, k, b, tiled); break;
+    case n: hipLaunchKernelGGL(gecko_encode_kernel<n>, grid, block, 0, s, k, b); break;
         HY_CASE(0) HY_CASE(1) HY_CASE(2) HY_CASE(3) HY_CASE(4) HY_CASE(5) HY_CASE(6) HY_CASE(7)
         HY_CASE(8) HY_CASE(9) HY_CASE(10) HY_CASE(11) HY_CASE(12) HY_CASE(13) HY_CASE(14) HY_CASE(15)
 #undef HY_CASE

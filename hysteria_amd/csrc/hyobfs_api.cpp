@@ -36,7 +36,7 @@ struct hyobfs_salamander {
     hipStream_t stream = nullptr;
     std::mutex mu;              // per-packet path, salt source, owned buffers (lk)
     uint64_t rng = 0;           // SplitMix64 state (RandSrc)
-    int kernel = 0;             // HYOBFS_KERNEL_* for batch launches
+    std::atomic<int> kernel{0}; // HYOBFS_KERNEL_* for batch launches (set_kernel may race batch calls)
     // per-packet staging in mapped pinned host memory: [in | out | salt | len | total]
     uint8_t* stage = nullptr;
     uint8_t* stage_dev = nullptr;
@@ -215,7 +215,7 @@ size_t run_one(hyobfs_salamander* c, bool obf, const uint8_t* in, size_t in_len,
     uint32_t* h_len = reinterpret_cast<uint32_t*>(h_misc + 8);
     *h_len = 0xFFFFFFFFu;
     BatchParams b{};
-    b.kernel = c->kernel;
+    b.kernel = c->kernel.load(std::memory_order_relaxed);
     b.n = 1;
     b.in = c->stage_dev;
     b.len_uniform = (uint32_t)in_len;
@@ -273,7 +273,7 @@ int fill_params(hyobfs_salamander* c, const hyobfs_batch* b, bool obf, BatchPara
     bp.out_off = b->out_off;
     bp.out_len = b->out_len;
     bp.out_total = reinterpret_cast<unsigned long long*>(b->out_total);
-    bp.kernel = c->kernel;
+    bp.kernel = c->kernel.load(std::memory_order_relaxed);
     // device scratch: the caller's workspace, or (run_batch) the context's pool
     const uint64_t need = hyobfs::batch_workspace_bytes(obf, bp);
     if (need && b->workspace) {
@@ -467,6 +467,11 @@ int hyobfs_device_count(void) {
     return n;
 }
 
+int hyobfs_device_pci_bus_id(int device, char* buf, int len) {
+    if (!buf || len < 13 || device < 0 || device >= hyobfs_device_count()) return HYOBFS_ERR_INVALID;
+    return hipDeviceGetPCIBusId(buf, len, device) == hipSuccess ? HYOBFS_OK : HYOBFS_ERR_HIP;
+}
+
 int hyobfs_salamander_new(const uint8_t* psk, size_t psk_len, int device, hyobfs_salamander** out) {
     if (!out) return HYOBFS_ERR_INVALID;
     if (psk_len < HYOBFS_PSK_MIN_LEN) return HYOBFS_ERR_PSK_TOO_SHORT;   // salamander.go:35-37
@@ -534,8 +539,8 @@ void hyobfs_salamander_free(hyobfs_salamander* c) { hyobfs::ctx_release(c); }
 int hyobfs_salamander_device(const hyobfs_salamander* c) { return c ? c->device : -1; }
 
 int hyobfs_salamander_set_kernel(hyobfs_salamander* c, int kernel) {
-    if (!c || kernel < HYOBFS_KERNEL_AUTO || kernel > HYOBFS_KERNEL_STREAM) return HYOBFS_ERR_INVALID;
-    c->kernel = kernel;
+    if (!c || kernel < HYOBFS_KERNEL_AUTO || kernel > HYOBFS_KERNEL_TILE) return HYOBFS_ERR_INVALID;
+    c->kernel.store(kernel, std::memory_order_relaxed);
     return HYOBFS_OK;
 }
 
@@ -624,7 +629,7 @@ uint64_t hyobfs_batch_workspace_bytes(const hyobfs_batch* b) {
     bp.out_stride = b->out_stride;
     // the largest need over the kernel choices: independent of the context's
     uint64_t m = 0;
-    for (int k : {hyobfs::kKernelAuto, hyobfs::kKernelWave, hyobfs::kKernelStream}) {
+    for (int k : {hyobfs::kKernelAuto, hyobfs::kKernelWave}) {
         bp.kernel = k;
         const uint64_t v = hyobfs::batch_workspace_bytes(true, bp);
         m = v > m ? v : m;
@@ -684,10 +689,6 @@ int hyobfs_shard_bounds(const uint32_t* in_len, uint64_t n, int nshards, uint64_
 // the encode kernel derives keys in registers: no workspace
 uint64_t hyobfs_gecko_workspace_size(uint64_t) { return 0; }
 
-uint64_t hyobfs_gecko_workspace_bytes(const hyobfs_gecko_batch* b) {
-    return b ? hyobfs::gecko_tiles_workspace_bytes(b->out_cap) : 0;
-}
-
 int hyobfs_gecko_encode_batch(hyobfs_salamander* c, const hyobfs_gecko_batch* b, void* stream) {
     if (!c || !b) return HYOBFS_ERR_INVALID;
     if (b->n == 0) return HYOBFS_OK;
@@ -699,24 +700,9 @@ int hyobfs_gecko_encode_batch(hyobfs_salamander* c, const hyobfs_gecko_batch* b,
     bool zero_key = true;
     for (int i = 0; i < 32; ++i) zero_key = zero_key && b->pad_key[i] == 0;
     if (zero_key) return HYOBFS_ERR_INVALID;
-    // the wire-tile kernel only when asked for (HYOBFS_KERNEL_STREAM): on the benchmark's
-    // frames it is slower than the wave-group kernel (profiles/r04_abg_gecko_*.txt)
-    const bool tiles = hyobfs::resolve_kernel(c->kernel) == hyobfs::kKernelStream;
-    const uint64_t ws_need = tiles ? hyobfs_gecko_workspace_bytes(b) : 0;
-    if (ws_need && b->workspace && b->workspace_bytes < ws_need) return HYOBFS_ERR_INVALID;
     DeviceGuard g(c->device);
     if (!g.ok) return HYOBFS_ERR_HIP;
-    hipStream_t s = static_cast<hipStream_t>(stream);
-    void* ws = ws_need ? b->workspace : nullptr;
-    void* scratch = nullptr;
-    if (ws_need && !ws) {   // the context's pool, freed behind the launch in stream order
-        hipMemPool_t pool = scratch_pool(c);
-        if (!pool) return HYOBFS_ERR_HIP;
-        if (hipMallocFromPoolAsync(&scratch, ws_need, pool, s) != hipSuccess) return HYOBFS_ERR_NOMEM;
-        ws = scratch;
-    }
-    const hipError_t e = hyobfs::launch_gecko_encode(c->kp, *b, tiles ? ws : nullptr, s);
-    if (scratch && hipFreeAsync(scratch, s) != hipSuccess) return HYOBFS_ERR_HIP;
+    const hipError_t e = hyobfs::launch_gecko_encode(c->kp, *b, static_cast<hipStream_t>(stream));
     return e == hipSuccess ? HYOBFS_OK : HYOBFS_ERR_HIP;
 }
 

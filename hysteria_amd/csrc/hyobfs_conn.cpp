@@ -142,11 +142,17 @@ int hyobfs_conn_close(hyobfs_conn* c) {
     return rc == 0 ? HYOBFS_OK : HYOBFS_ERR_IO;
 }
 
+// A connection freed without Close (a Go finalizer on a dropped gpuPacketConn)
+// closes its descriptor too: the connection owns the fd from hyobfs_conn_wrap on,
+// as Go's UDPConn closes its fd from its own finalizer.
 void hyobfs_conn_free(hyobfs_conn* c) {
     if (!c) return;
     {
         std::lock_guard<std::mutex> lk(c->life_mu);
-        if (!c->closing.load(std::memory_order_seq_cst)) quiesce(c, false);   // detach: the socket stays open
+        if (!c->closing.load(std::memory_order_seq_cst)) {
+            quiesce(c, false);   // the coalescer sends what write_to accepted first
+            (void)close(c->fd);
+        }
     }
     hyobfs::coalescer_free(c->co);   // (already stopped)
     c->rx.release();

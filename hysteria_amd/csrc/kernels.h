@@ -32,7 +32,7 @@ constexpr int kTile = 256;          // datagrams per tile-sum entry of the packe
 constexpr uint32_t kMaxDatagram = (1u << 24) - 64;  // longest datagram a batch accepts
 constexpr uint64_t kMaxStride = 1ull << 24;         // longest slot of a slotted output
 // batch kernels (include/hyobfs.h HYOBFS_KERNEL_*)
-constexpr int kKernelAuto = 0, kKernelWave = 1, kKernelTile = 2, kKernelStream = 3;
+constexpr int kKernelAuto = 0, kKernelWave = 1, kKernelTile = 2;
 
 // BLAKE2b state for the per-packet key, precomputed on the host from the PSK
 // alone (salamander.go:88-91 hashes PSK || salt; every block before the one
@@ -78,7 +78,7 @@ struct BatchParams {
 // HYOBFS_KERNEL environment variable, else 0)
 int resolve_kernel(int ctx_kernel);
 hipError_t launch_salamander(bool obfuscate, const BatchParams& b, const KeyParams& k, hipStream_t s);
-// the kernel launch_salamander would run (kKernelTile / kKernelWave / kKernelStream;
+// the kernel launch_salamander would run (kKernelTile / kKernelWave;
 // kKernelAuto for an empty batch)
 int batch_kernel(bool obfuscate, const BatchParams& b);
 // device scratch a launch of this batch needs (0: none); launch_salamander takes it
@@ -88,10 +88,7 @@ uint64_t batch_workspace_bytes(bool obfuscate, const BatchParams& b);
 inline bool contiguous_input(const BatchParams& b) { return !b.in_off && b.in_stride == 0 && b.in_len && b.n > 1; }
 hipError_t launch_keys(const KeyParams& k, const uint64_t* salts, uint8_t* keys, uint64_t n,
                        hipStream_t s);
-// ws: gecko_tiles_workspace_bytes(b.out_cap) bytes (NULL or out_cap 0: the wave-group kernel only)
-// ws: the wire-tile kernel's scratch (gecko_tiles_workspace_bytes), NULL = the wave-group kernel
-hipError_t launch_gecko_encode(const KeyParams& k, const hyobfs_gecko_batch& b, void* ws, hipStream_t s);
-uint64_t gecko_tiles_workspace_bytes(uint64_t out_cap);
+hipError_t launch_gecko_encode(const KeyParams& k, const hyobfs_gecko_batch& b, hipStream_t s);
 hipError_t launch_gecko_parse(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint64_t n,
                               hyobfs_gecko_parsed* out, hipStream_t s);
 hipError_t launch_synth_stream(uint8_t* dst, uint64_t nbytes, uint64_t seed, uint64_t start,

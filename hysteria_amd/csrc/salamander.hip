@@ -13,7 +13,7 @@
 //     One-shot workgroups of 16 datagrams: a key wave beside three data waves.
 //   * salamander_wave_kernel (salamander_wave.h): every other layout (packed
 //     output, ragged lengths, any alignment).  One wave per 64-datagram group.
-#include "salamander_stream.h"
+#include "salamander_tile.h"
 
 namespace hyobfs {
 
@@ -26,11 +26,7 @@ namespace hyobfs {
     extern template void launch_tile_sw<true, n>(const BatchParams&, const KeyParams&, const TileParams&,   \
                                                  hipStream_t);                                              \
     extern template void launch_tile_sw<false, n>(const BatchParams&, const KeyParams&, const TileParams&,  \
-                                                  hipStream_t);                                             \
-    extern template void launch_stream_sw<true, n>(const BatchParams&, const KeyParams&, const StreamParams&, \
-                                                   hipStream_t);                                            \
-    extern template void launch_stream_sw<false, n>(const BatchParams&, const KeyParams&, const StreamParams&, \
-                                                    hipStream_t);
+                                                  hipStream_t);
 HY_EXTERN_SW(0) HY_EXTERN_SW(1) HY_EXTERN_SW(2) HY_EXTERN_SW(3) HY_EXTERN_SW(4) HY_EXTERN_SW(5)
 HY_EXTERN_SW(6) HY_EXTERN_SW(7) HY_EXTERN_SW(8) HY_EXTERN_SW(9) HY_EXTERN_SW(10) HY_EXTERN_SW(11)
 HY_EXTERN_SW(12) HY_EXTERN_SW(13) HY_EXTERN_SW(14) HY_EXTERN_SW(15)
@@ -124,6 +120,29 @@ __global__ __launch_bounds__(1024) void scan_tiles_kernel(uint64_t* v, uint64_t*
     if (t == 0) arr[ntiles] = s_carry;
 }
 
+// Contiguous input run on a kernel that takes explicit offsets (slotted output, or
+// packed runs shorter than 64): in_off[i] from the scanned per-tile length sums and
+// a wave scan.  Wave w of workgroup b owns tile 4b + w, four datagrams per lane.
+__global__ __launch_bounds__(256) void in_offsets_kernel(BatchParams B, uint64_t* in_off) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t tile = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (tile * kTile >= B.n) return;   // whole waves
+    const uint64_t p0 = tile * kTile + 4ull * lane;
+    uint32_t L[4];
+    uint64_t sl = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        L[k] = p0 + k < B.n ? B.in_len[p0 + k] : 0u;
+        sl += L[k];
+    }
+    uint64_t x = B.in_tile_prefix[tile] + wave_incl_scan(sl, (int)lane) - sl;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        if (p0 + k < B.n) in_off[p0 + k] = x;
+        x += L[k];
+    }
+}
+
 // keys only (hyobfs_salamander_key): key[i] = BLAKE2b-256(PSK || salts[i])
 __global__ __launch_bounds__(256) void keys_kernel(KeyParams K, const uint64_t* salts, uint8_t* keys,
                                                    uint64_t n) {
@@ -178,18 +197,14 @@ __global__ void synth_bimodal_kernel(uint32_t* dst, uint64_t n, uint64_t seed, u
 
 // Kernel choice ("Kernels"): AUTO runs the tile kernel where it
 // applies (tile_params) and the wave kernel elsewhere; WAVE forces the wave
-// kernel; TILE asks for the tile kernel (falls back to the wave kernel where it
-// does not apply); STREAM asks for the stream kernel on contiguous packed input
-// (the wave kernel elsewhere).  HYOBFS_KERNEL=wave|tile|stream sets what AUTO
-// means in a process.
+// kernel; TILE is AUTO.  HYOBFS_KERNEL=wave|tile sets what AUTO means in a process.
 static int kernel_override() {   // HYOBFS_KERNEL, as HYOBFS_KERNEL_* (0 = auto); read once, thread-safe
     static const int v = [] {
         const char* e = std::getenv("HYOBFS_KERNEL");
-        return !e                          ? kKernelAuto
-               : std::strcmp(e, "wave") == 0   ? kKernelWave
-               : std::strcmp(e, "tile") == 0   ? kKernelTile
-               : std::strcmp(e, "stream") == 0 ? kKernelStream
-                                               : kKernelAuto;
+        return !e                        ? kKernelAuto
+               : std::strcmp(e, "wave") == 0 ? kKernelWave
+               : std::strcmp(e, "tile") == 0 ? kKernelTile
+                                             : kKernelAuto;
     }();
     return v;
 }
@@ -221,38 +236,28 @@ static void launch_main(const BatchParams& bp, const KeyParams& k, hipStream_t s
     }
 }
 
-// Contiguous input.  Packed output: the wave kernel, which takes the input offsets
-// from a scan of the lengths done with the widths' (tile_sums_kernel,
-// scan_tiles_kernel); the stream kernel (salamander_stream.h) when asked for
-// (HYOBFS_KERNEL_STREAM) and the input is 16-byte aligned (LDS-DMA moves 16-byte
-// chunks).  Slotted output, or wave runs shorter than 64: the stream prepass writes
-// the input offsets and the kernels for explicit offsets run on them.
-// (configs[2], one process: the stream kernel 1.89 ms, the wave kernel on offsets
-// 1.46 ms, profiles/r04_ab_bimodal_*.txt.)
-static bool stream_eligible(const BatchParams& b) {
-    return contiguous_input(b) && b.out_stride == 0 && resolve_kernel(b.kernel) == kKernelStream &&
-           (reinterpret_cast<uintptr_t>(b.in) & 15u) == 0;
-}
+// Contiguous input.  Packed output in runs of 64 (the default): the wave kernel takes
+// its input offsets from a scan of the lengths done with the widths'
+// (tile_sums_kernel, scan_tiles_kernel).  Otherwise (slotted output, shorter packed
+// runs) a prepass writes the input offsets into the scratch -- length sums, their
+// scan, in_offsets_kernel -- and the kernels for explicit offsets run on them.
 static bool wave_scans_input(const BatchParams& b) {   // the wave kernel scans the lengths itself
-    return contiguous_input(b) && b.out_stride == 0 && !stream_eligible(b) && wave_packed_run_log2() == 6;
+    return contiguous_input(b) && b.out_stride == 0 && wave_packed_run_log2() == 6;
 }
 
-static uint64_t align16(uint64_t x) { return (x + 15) & ~15ull; }
-
+// scratch: [width sums | length sums] (ntiles + 1 each), then, when the prepass
+// writes them, the input offsets (8 B per datagram)
 uint64_t batch_workspace_bytes(bool obf, const BatchParams& b) {
     (void)obf;
     if (b.n == 0) return 0;
     const uint64_t tsums = (div_up(b.n, kTile) + 1) * 8;
     if (!contiguous_input(b)) return b.out_stride == 0 ? tsums : 0;
-    if (stream_eligible(b)) return stream_workspace_bytes(b.n, b.out_cap, true, false);
-    if (wave_scans_input(b)) return 2 * tsums;
-    return align16(stream_workspace_bytes(b.n, 0, false, true)) + (b.out_stride == 0 ? tsums : 0);
+    return 2 * tsums + (wave_scans_input(b) ? 0 : 8 * b.n);
 }
 
 // Which kernel launch_salamander runs for this batch (HYOBFS_KERNEL_*; no launch).
 int batch_kernel(bool obf, const BatchParams& b) {
     if (b.n == 0) return kKernelAuto;   // nothing runs
-    if (stream_eligible(b)) return kKernelStream;
     TileParams T;
     BatchParams bp = b;
     if (contiguous_input(b) && !wave_scans_input(b))
@@ -263,33 +268,21 @@ int batch_kernel(bool obf, const BatchParams& b) {
 }
 
 template <bool OBF>
-static hipError_t launch_contiguous(BatchParams& bp, const KeyParams& k, hipStream_t s, bool& done) {
-    done = false;
+static hipError_t launch_contiguous(BatchParams& bp, hipStream_t s) {
     if (!bp.scratch) return hipErrorInvalidValue;
-    StreamParams S;
-    if (stream_eligible(bp)) {
-        launch_stream_prepass<OBF>(bp, S, bp.scratch, true, false, s);
-        switch (k.salt_pos >> 3) {
-#define HY_CASE(n) \
-    case n: launch_stream_sw<OBF, n>(bp, k, S, s); break;
-            HY_CASE(0) HY_CASE(1) HY_CASE(2) HY_CASE(3) HY_CASE(4) HY_CASE(5) HY_CASE(6) HY_CASE(7)
-            HY_CASE(8) HY_CASE(9) HY_CASE(10) HY_CASE(11) HY_CASE(12) HY_CASE(13) HY_CASE(14)
-            HY_CASE(15)
-#undef HY_CASE
-        }
-        done = true;
-        return hipGetLastError();
-    }
-    if (wave_scans_input(bp)) {   // the length sums follow the width sums in the scratch
-        bp.tile_sums = static_cast<uint64_t*>(bp.scratch);
-        bp.in_tile_sums = bp.tile_sums + div_up(bp.n, kTile) + 1;
-        return hipSuccess;
-    }
-    launch_stream_prepass<OBF>(bp, S, bp.scratch, false, true, s);
-    bp.in_off = S.in_off_out;
-    if (bp.out_stride == 0)
-        bp.tile_sums = reinterpret_cast<uint64_t*>(static_cast<uint8_t*>(bp.scratch) +
-                                                   align16(stream_workspace_bytes(bp.n, 0, false, true)));
+    const uint64_t ntiles = div_up(bp.n, kTile);
+    bp.tile_sums = static_cast<uint64_t*>(bp.scratch);
+    bp.in_tile_sums = bp.tile_sums + ntiles + 1;
+    if (wave_scans_input(bp)) return hipSuccess;   // the packed launch below scans both sums
+    uint64_t* in_off = bp.in_tile_sums + ntiles + 1;
+    const dim3 grid((uint32_t)div_up(ntiles, 4)), block(256);
+    hipLaunchKernelGGL(tile_sums_kernel<OBF>, grid, block, 0, s, bp, ntiles);
+    hipLaunchKernelGGL(scan_tiles_kernel, dim3(1), dim3(1024), 0, s, bp.in_tile_sums, nullptr, ntiles);
+    bp.in_tile_prefix = bp.in_tile_sums;
+    hipLaunchKernelGGL(in_offsets_kernel, grid, block, 0, s, bp, in_off);
+    bp.in_off = in_off;   // from here on an ordinary batch with explicit offsets
+    bp.in_tile_sums = nullptr;
+    bp.in_tile_prefix = nullptr;
     return hipGetLastError();
 }
 
@@ -300,9 +293,8 @@ hipError_t launch_salamander(bool obf, const BatchParams& b, const KeyParams& k,
     if (k.nblk == 2 && (k.salt_pos >> 3) != 15) return hipErrorInvalidValue;   // by construction
     BatchParams bp = b;
     if (contiguous_input(b)) {
-        bool done = false;
-        const hipError_t e = obf ? launch_contiguous<true>(bp, k, s, done) : launch_contiguous<false>(bp, k, s, done);
-        if (e != hipSuccess || done) return e;
+        const hipError_t e = obf ? launch_contiguous<true>(bp, s) : launch_contiguous<false>(bp, s);
+        if (e != hipSuccess) return e;
     }
     if (bp.out_stride == 0) {
         if (!bp.tile_sums) return hipErrorInvalidValue;

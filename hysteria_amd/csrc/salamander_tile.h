@@ -262,6 +262,34 @@ __device__ __forceinline__ void glds16(const uint8_t* g, uint8_t* l) {   // LDS-
 #endif
 }
 
+#ifndef HY_TILE_PREFETCH
+#define HY_TILE_PREFETCH 2
+#endif
+#ifndef HY_TILE_PF_PHASE
+#define HY_TILE_PF_PHASE 0
+#endif
+#ifndef HY_TILE_COMPOSE
+#define HY_TILE_COMPOSE 1
+#endif
+
+// One 8-byte half of an output chunk: datagram q, slot offset rr.  Branch-free:
+// every lane does one data read and one key read from LDS whatever the half holds
+// (salt: data = the salt, key masked off; payload: 8 staged bytes and the key word;
+// outside the region: reads of word 0, not stored), so a wave never splits on the
+// one salt / datagram-edge chunk per datagram.
+template <bool OBF>
+__device__ __forceinline__ uint64_t tile_half(const uint8_t* s_in, const uint64_t* s_key, const uint64_t* s_salt,
+                                              uint32_t q, uint32_t rr, bool valid, uint32_t in_stride) {
+    constexpr uint32_t SALT = OBF ? 8u : 0u, SKIP = OBF ? 0u : 8u;
+    const bool salt = OBF && rr < 8u;
+    const uint32_t j = rr - SALT;   // payload offset (wraps for the salt; unused then)
+    const uint32_t qq = valid ? q : 0u;
+    const uint64_t* d = salt ? s_salt + qq
+                             : reinterpret_cast<const uint64_t*>(s_in + (valid ? q * in_stride + SKIP + j : 0u));
+    const uint64_t k = s_key[qq * 8u + ((j >> 3) & 3u)];
+    return *d ^ (salt ? 0ull : k);
+}
+
 template <bool OBF, int SW>
 __global__ __launch_bounds__(256, HY_TILE_MIN_WAVES) void salamander_tile_kernel(BatchParams B, KeyParams K,
                                                                                   TileParams T) {
@@ -289,8 +317,20 @@ __global__ __launch_bounds__(256, HY_TILE_MIN_WAVES) void salamander_tile_kernel
         // ---- the key wave: salts, BLAKE2b-256 on quads (lane 4k+i: word i of key k), LDS
         const uint32_t qk = lane >> 2, qi = lane & 3;
         uint64_t salt = 0;
+#ifdef HY_TILE_ABL_SALT
+        salt = p0 + qk;
+#else
         if (qk < nt) salt = OBF ? B.salts[p0 + qk] : load8_wire_salt(ib + qk * in_stride);
+#endif
+#if HY_TILE_PREFETCH
+        uint32_t pf = 0;
+        if (OBF && qk < nt && qi < HY_TILE_PREFETCH)
+            pf = *reinterpret_cast<const uint32_t*>(ib + qk * in_stride + (((2 * qi + HY_TILE_PF_PHASE) * in_stride / (2 * HY_TILE_PREFETCH)) & ~127u));
+#endif
         const uint64_t kw = quad_key<SW>(K, salt, qi);
+#if HY_TILE_PREFETCH && !defined(HYOBFS_EMULATE)
+        asm volatile("" ::"v"(pf));
+#endif
         if (qk < nt) {
             s_key[qk * 8 + qi] = kw;
             s_key[qk * 8 + 4 + qi] = kw;
@@ -342,6 +382,12 @@ __global__ __launch_bounds__(256, HY_TILE_MIN_WAVES) void salamander_tile_kernel
                 ++p2;
             }
             const bool vlo = (uint32_t)r < W, vhi = p2 < nt && r2 < W;
+#if HY_TILE_COMPOSE == 1
+            st[u] = (vlo ? 1u : 0u) | (vhi ? 2u : 0u);
+            lo[u] = tile_half<OBF>(s_in, s_key, s_salt, p, (uint32_t)r, vlo, in_stride);
+            hi[u] = tile_half<OBF>(s_in, s_key, s_salt, p2, r2, vhi, in_stride);
+            continue;
+#endif
             const bool slo = OBF && (uint32_t)r < 8u, shi = OBF && r2 < 8u;
             const uint32_t jlo = (uint32_t)r - SALT, jhi = r2 - SALT;
             const uint32_t alo = p * in_stride + SKIP + jlo, ahi = p2 * in_stride + SKIP + jhi;
@@ -404,7 +450,7 @@ inline bool tile_params(const BatchParams& b, TileParams& T) {
 // 74.5-74.7 %: launch gaps); 1M is kept so that the 1M-datagram bench batch stays one
 // launch, whose HIP-event time and rocprofv3 kernel average describe the same thing.
 #ifndef HY_TILE_LAUNCH_TILES
-#define HY_TILE_LAUNCH_TILES 65536   // 1M datagrams
+#define HY_TILE_LAUNCH_TILES 32768   // 512K datagrams
 #endif
 inline uint64_t tile_launch_tiles() {   // read once, thread-safe (a function-local static)
     static const uint64_t v = [] {

@@ -101,7 +101,6 @@ def _glib(lib=None):
                 ("hyobfs_gecko_decode_frame", i32, [vp, sz, hp, ctypes.POINTER(sz)]),
                 ("hyobfs_gecko_pad_len", u32, [i32, i32, u32, u32]),
                 ("hyobfs_gecko_workspace_size", u64, [u64]),
-                ("hyobfs_gecko_workspace_bytes", u64, [ctypes.POINTER(HyobfsGeckoBatch)]),
                 ("hyobfs_gecko_encode_batch", i32, [vp, ctypes.POINTER(HyobfsGeckoBatch), vp]),
                 ("hyobfs_gecko_parse_batch", i32, [vp, vp, vp, u64, vp, vp]),
                 ("hyobfs_gecko_random_pad_key", i32, [vp, vp])):
@@ -386,11 +385,6 @@ def workspace_size(n: int) -> int:
     return int(_glib().hyobfs_gecko_workspace_size(n))
 
 
-def workspace_bytes(out_cap: int) -> int:
-    """hyobfs_gecko_workspace_bytes: scratch of the wire-tile path for ``out_cap`` bytes of wire."""
-    return int(_glib().hyobfs_gecko_workspace_bytes(ctypes.byref(HyobfsGeckoBatch(out_cap=out_cap))))
-
-
 def random_pad_key() -> tuple[bytes, bytes]:
     """A fresh (key, nonce) for the padding keystream from the OS (hyobfs_gecko_random_pad_key,
     getrandom: the source of the reference's crypto/rand)."""
@@ -400,26 +394,15 @@ def random_pad_key() -> tuple[bytes, bytes]:
 
 
 def encode_batch(obfuscator, *, msg, frames, salts, out, out_off, pad_key: bytes | None = None,
-                 pad_nonce: bytes | None = None, workspace=None, n=None, stream=None, out_cap=None,
-                 workspace_bytes=None) -> None:
+                 pad_nonce: bytes | None = None, workspace=None, n=None, stream=None) -> None:
     """hyobfs_gecko_encode_batch: every frame's wire datagram in one device pass.
-    Arguments are device tensors (torch) or device pointers.  ``out_cap`` (default:
-    the size of an ``out`` tensor, 0 for a pointer) lets frames placed in order run
-    the wire-tile kernel; its scratch comes from ``workspace`` (at least
-    ``workspace_bytes(out_cap)`` bytes) or, when None, the context's pool.  Padding is
-    a keyed keystream (include/hyobfs_gecko.h): a fresh OS-random key per call unless
-    pad_key and pad_nonce are given (reproducible output for tests)."""
+    Arguments are device tensors (torch) or device pointers; ``workspace`` is accepted
+    and ignored (ABI 3: no scratch).  Padding is a keyed keystream
+    (include/hyobfs_gecko.h): a fresh OS-random key per call unless pad_key and
+    pad_nonce are given (reproducible output for tests)."""
     from .salamander import _ptr, _stream
     if n is None:   # frames: 16-byte hyobfs_gecko_frame records
         n = frames.numel() * frames.element_size() // FRAME_DTYPE.itemsize if hasattr(frames, "numel") else len(frames)
-    if out_cap is None:
-        out_cap = out.numel() * out.element_size() if hasattr(out, "numel") else 0
-    ws_bytes = 0
-    if workspace is not None:
-        ws_bytes = workspace_bytes if workspace_bytes is not None else (
-            workspace.numel() * workspace.element_size() if hasattr(workspace, "numel") else 0)
-        if ws_bytes == 0:
-            workspace = None
     if pad_key is None or pad_nonce is None:
         pad_key, pad_nonce = random_pad_key()
     if len(pad_key) != 32 or len(pad_nonce) != 12:
@@ -427,8 +410,7 @@ def encode_batch(obfuscator, *, msg, frames, salts, out, out_off, pad_key: bytes
     b = HyobfsGeckoBatch(n=n, msg=_ptr(msg), frames=_ptr(frames), salts=_ptr(salts),
                          pad_key=(ctypes.c_uint8 * 32).from_buffer_copy(pad_key),
                          pad_nonce=(ctypes.c_uint8 * 12).from_buffer_copy(pad_nonce),
-                         out=_ptr(out), out_off=_ptr(out_off), workspace=_ptr(workspace), workspace_bytes=ws_bytes,
-                         out_cap=out_cap)
+                         out=_ptr(out), out_off=_ptr(out_off))
     lib = _glib(getattr(obfuscator, "_lib", None))   # the library the context came from
     check(lib.hyobfs_gecko_encode_batch(obfuscator._h, ctypes.byref(b), _stream(stream, out)), "gecko_encode_batch")
 

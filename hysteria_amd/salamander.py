@@ -136,12 +136,12 @@ class SalamanderObfuscator:
     def __exit__(self, *exc):
         self.close()
 
-    KERNELS = {"auto": 0, "wave": 1, "tile": 2, "stream": 3}
+    KERNELS = {"auto": 0, "wave": 1, "tile": 2}
 
     def set_kernel(self, kernel: str) -> None:
         """Batch kernel of this context: "auto" (the tile kernel where it applies, else the
-        wave-group kernel), "wave" (forced), "tile" or "stream" (contiguous packed input:
-        the stream kernel; include/hyobfs.h, HYOBFS_KERNEL_*)."""
+        wave-group kernel), "wave" (forced) or "tile" (= auto; include/hyobfs.h,
+        HYOBFS_KERNEL_*)."""
         check(self._lib.hyobfs_salamander_set_kernel(self._h, self.KERNELS[kernel]), "set_kernel")
         self.kernel = kernel
 
@@ -200,7 +200,7 @@ class SalamanderObfuscator:
         b = _make_batch(inp=inp, n=n, out=out, **kw)
         k = self._lib.hyobfs_salamander_batch_kernel(self._h, ctypes.byref(b), int(bool(obf)))
         check(min(k, 0), "batch_kernel")
-        return {0: "none", 1: "wave", 2: "tile", 3: "stream"}[k]
+        return {0: "none", 1: "wave", 2: "tile"}[k]
 
     @staticmethod
     def workspace_bytes(*, inp, n, out, **kw) -> int:
@@ -271,6 +271,13 @@ def deobfuscate_batch_sharded(obfuscators, shards) -> None:
 
 def device_count() -> int:
     return _lib.load().hyobfs_device_count()
+
+
+def device_pci_bus_id(device: int) -> str:
+    """hyobfs_device_pci_bus_id: the PCI bus id of HIP device ``device`` (which card)."""
+    buf = ctypes.create_string_buffer(64)
+    check(_lib.load().hyobfs_device_pci_bus_id(device, buf, 64), "device_pci_bus_id")
+    return buf.value.decode()
 
 
 def workspace_size(n: int) -> int:

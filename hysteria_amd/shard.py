@@ -9,6 +9,21 @@ from __future__ import annotations
 import numpy as np
 
 
+def check_rank_devices(bus_ids: list[str], device_count: int) -> bool:
+    """Device binding of a one-process-per-GPU job (bench.py): ``bus_ids[r]`` is the PCI
+    bus id rank r bound.  Returns True when two ranks share a card, which is only
+    allowed when the node has fewer cards than ranks (a rehearsal of N ranks on one
+    card); with enough cards it raises, since a shared card would silently halve
+    both ranks' rate in a scaling run."""
+    world = len(bus_ids)
+    shared = len(set(bus_ids)) < world
+    if shared and device_count >= world:
+        dup = sorted({b for b in bus_ids if bus_ids.count(b) > 1})
+        raise RuntimeError(f"{world} ranks on {device_count} visible devices, but ranks share {dup}: "
+                           "check LOCAL_RANK / HIP_VISIBLE_DEVICES")
+    return shared
+
+
 def even_split(n: int, world: int, rank: int) -> tuple[int, int]:
     """(first, count) of rank's contiguous share of n datagrams; counts differ by <= 1."""
     if world < 1 or not 0 <= rank < world:

@@ -56,16 +56,29 @@
 extern "C" {
 #endif
 
-/* ABI version.  2 (this header) against 1:
+/* ABI version.  3 (this header) against 2:
+ *   - HYOBFS_KERNEL_STREAM (3) is gone (the stream kernel lost to the wave-group
+ *     kernel on every measured layout); hyobfs_salamander_set_kernel rejects 3;
+ *   - hyobfs_gecko_workspace_bytes is gone, and hyobfs_gecko_batch's workspace,
+ *     workspace_bytes and out_cap are ignored (the Gecko wire-tile kernel is gone);
+ *   - contiguous input with slotted output needs 2 x hyobfs_batch_workspace_size(n)
+ *     + 8 n bytes of scratch (was 8 n + block sums): ask hyobfs_batch_workspace_bytes;
+ *   - new: hyobfs_device_pci_bus_id.
+ * 2 against 1:
  *   - struct hyobfs_gecko_batch: pad_seed (u64) became pad_key[32], pad_nonce[12]
  *     and reserved_ (hyobfs_gecko.h), so the fields after it moved;
  *   - HYOBFS_KERNEL_* values: 2 is TILE (was PERSISTENT), 3..6 are rejected;
  *   - hyobfs_conn_close no longer frees the connection: hyobfs_conn_free does
  *     (include/hyobfs_conn.h), and calls after close fail with EBADF;
- *   - new status HYOBFS_ERR_CLOSED; a zero Gecko pad key is rejected.
+ *   - new status HYOBFS_ERR_CLOSED; a zero Gecko pad key is rejected;
+ *   - CONTIGUOUS input (struct hyobfs_batch): in_off == NULL, in_stride == 0 and
+ *     in_len != NULL now put the datagrams back to back.  In ABI 1 the same fields
+ *     put every datagram at `in`.  With in_len == NULL (len_uniform), in_stride 0
+ *     still means "every datagram at in".  A v1 caller that relied on that must
+ *     pass in_off (all zeros) instead.
  * Bindings compare hyobfs_abi_version() with the version they were written
  * for and refuse a mismatch (hysteria_amd/_lib.py does). */
-#define HYOBFS_ABI_VERSION 2
+#define HYOBFS_ABI_VERSION 3
 
 #define HYOBFS_PSK_MIN_LEN 4  /* smPSKMinLen, salamander.go:14 */
 #define HYOBFS_SALT_LEN 8     /* smSaltLen,   salamander.go:15 */
@@ -93,6 +106,9 @@ const char* hyobfs_build_id(void);
 const char* hyobfs_status_string(int status);
 /* number of HIP devices visible to this process (0 when none) */
 int hyobfs_device_count(void);
+/* PCI bus id of HIP device `device` ("dddd:bb:dd.f", NUL-terminated, len >= 13):
+   which physical card a process bound (bench.py records it per rank). */
+int hyobfs_device_pci_bus_id(int device, char* buf, int len);
 
 /* ------------------------------------------------------------- lifecycle */
 /* newSalamanderObfuscator (salamander.go:34-46) + GPU binding.  Copies the
@@ -109,21 +125,19 @@ int hyobfs_salamander_device(const hyobfs_salamander* ctx);
 /* Batch kernel of this context (no reference counterpart: a tuning knob).
    HYOBFS_KERNEL_AUTO runs the tile kernel on slotted batches whose region edges
    are all multiples of 8 (one length, slot and input stride multiples of 8,
-   payloads of 16 bytes or more, nothing dropped, no 16-byte chunk holding two
-   datagrams' payload bytes) -- the uniform 1200-byte batch of the benchmark --
-   and the wave-group kernel on every other batch (packed output, ragged
-   lengths, any alignment; contiguous input scans its lengths alongside the
-   widths).  HYOBFS_KERNEL_WAVE forces the wave-group kernel; HYOBFS_KERNEL_TILE
-   is AUTO; HYOBFS_KERNEL_STREAM runs the stream kernel on contiguous input with
-   packed output and a 16-byte aligned `in` (AUTO elsewhere; slower than AUTO on
-   the benchmark's mix today, kept for tuning).  The HYOBFS_KERNEL environment
-   variable (wave|tile|stream) overrides AUTO.  Returns HYOBFS_ERR_INVALID for an
-   unknown value.  Outputs are identical. */
+   payloads of 16 bytes or more, nothing dropped) -- the uniform 1200-byte batch
+   of the benchmark -- and the wave-group kernel on every other batch (packed
+   output, ragged lengths, any alignment; contiguous input scans its lengths
+   alongside the widths).  HYOBFS_KERNEL_WAVE forces the wave-group kernel;
+   HYOBFS_KERNEL_TILE is AUTO.  The HYOBFS_KERNEL environment variable
+   (wave|tile) overrides AUTO.  Returns HYOBFS_ERR_INVALID for an unknown value.
+   May be called while other threads run batches on the context (an atomic
+   setting; a batch uses the value it read when it started).  Outputs are
+   identical. */
 enum {
     HYOBFS_KERNEL_AUTO = 0,
     HYOBFS_KERNEL_WAVE = 1,
-    HYOBFS_KERNEL_TILE = 2,
-    HYOBFS_KERNEL_STREAM = 3
+    HYOBFS_KERNEL_TILE = 2
 };
 int hyobfs_salamander_set_kernel(hyobfs_salamander* ctx, int kernel);
 
@@ -162,8 +176,8 @@ size_t hyobfs_salamander_deobfuscate(hyobfs_salamander* ctx, const uint8_t* in,
  *             bytes at in + (in_off ? in_off[i] : i * in_stride)       (any alignment)
  *             CONTIGUOUS input: in_off == NULL, in_stride == 0 and in_len != NULL
  *             put datagram i at in + L_0 + ... + L_{i-1} (back to back; no
- *             offset array; with HYOBFS_KERNEL_STREAM and a 16-byte aligned
- *             `in`, packed output runs the stream kernel)
+ *             offset array).  Without in_len, in_stride == 0 puts every
+ *             datagram at `in`.
  *   salt    : obfuscate only: salts[i], 8 bytes, little-endian u64
  *             (salt byte b = (salts[i] >> 8b) & 0xff)
  *   output  : W_i = L_i + 8 (obfuscate) or L_i - 8 (deobfuscate)
@@ -211,14 +225,13 @@ typedef struct hyobfs_batch {
 /* Scratch of a packed batch with explicit or strided input offsets: (ceil(n/256)+1) x 8. */
 uint64_t hyobfs_batch_workspace_size(uint64_t n);
 /* Scratch any batch needs, whatever the kernel choice: the above for packed
-   batches with explicit offsets; for contiguous input with packed output twice
-   that (width and length sums) or, for the stream kernel, its prepass's block
-   sums (16 B per 1024 datagrams) and tile descriptors (32 B per 16 KiB of
-   out_cap); slotted output with contiguous input: input offsets (8 B per
-   datagram); 0 for other slotted batches. */
+   batches with explicit offsets; for contiguous input twice that (width and
+   length sums), plus 8 B per datagram (the input offsets a prepass writes) when
+   the output is slotted or HYOBFS_PACKED_RUN_LOG2 shortens the packed runs; 0 for
+   other slotted batches. */
 uint64_t hyobfs_batch_workspace_bytes(const hyobfs_batch* b);
 /* Which batch kernel a call with this batch would run under the context's
-   setting (HYOBFS_KERNEL_TILE, _WAVE or _STREAM; HYOBFS_KERNEL_AUTO for an
+   setting (HYOBFS_KERNEL_TILE or _WAVE; HYOBFS_KERNEL_AUTO for an
    empty batch), or a negative status for an invalid batch.  No device work:
    tests use it to prove which kernel their case exercised. */
 int hyobfs_salamander_batch_kernel(hyobfs_salamander* ctx, const hyobfs_batch* b, int obfuscate);

@@ -51,9 +51,11 @@ typedef struct hyobfs_dgram {
     uint32_t pad_;
 } hyobfs_dgram;
 
-/* Wrap a bound UDP socket.  The connection takes a reference on ctx (released
-   by hyobfs_conn_free).  batch = the largest number of datagrams per batched
-   call (0 = 1024). */
+/* Wrap a bound UDP socket.  The connection owns fd from here on: hyobfs_conn_close,
+   or hyobfs_conn_free on a connection that was not closed, closes it (a binding
+   that keeps its own socket passes a dup).  The connection takes a reference on
+   ctx (released by hyobfs_conn_free).  batch = the largest number of datagrams per
+   batched call (0 = 1024). */
 int hyobfs_conn_wrap(int fd, hyobfs_salamander* ctx, uint32_t batch, hyobfs_conn** out);
 /* Close() (conn.go:101-103): shuts the connection down but does NOT free it.
    A coalescing connection first sends every datagram write_to accepted; every
@@ -66,8 +68,9 @@ int hyobfs_conn_wrap(int fd, hyobfs_salamander* ctx, uint32_t batch, hyobfs_conn
 int hyobfs_conn_close(hyobfs_conn* c);
 /* Frees the connection and releases its context reference.  No call on c may
    be in progress or start later (a Go finalizer has exactly that guarantee).
-   On a connection that was not closed it detaches first: the coalescer sends
-   what was accepted, its threads stop, and the socket stays open. */
+   On a connection that was not closed it shuts down first: the coalescer sends
+   what was accepted, its threads stop, and the socket is closed (the fd is the
+   connection's, as a Go UDPConn's finalizer closes its own). */
 void hyobfs_conn_free(hyobfs_conn* c);
 
 /* ReadFrom: bytes written to p (>= 0), or -1 with errno set (socket error). */

@@ -113,25 +113,13 @@ typedef struct hyobfs_gecko_batch {
     uint8_t* out;                        /* device */
     const uint64_t* out_off;             /* frame i's wire datagram at out + out_off[i] (device);
                                             its length is 8 + 5 + pad_len + chunk_len */
-    void* workspace;                     /* >= hyobfs_gecko_workspace_bytes(b) bytes (device), or NULL:
-                                            then the context's stream-ordered pool provides it */
-    uint64_t workspace_bytes;
-    /* Bytes of `out` the frames lie in (0: not given).  With the context's kernel set
-       to HYOBFS_KERNEL_STREAM, out_cap given, and every frame valid and placed after
-       the one before it (back to back or with gaps, what writeFragmented produces),
-       the wire-tile kernel runs: 16 KiB tiles of `out`, each written whole by one
-       workgroup.  Otherwise the wave-group kernel runs (the default: faster on the
-       benchmark's frames today); the output is the same. */
-    uint64_t out_cap;
+    void* workspace;                     /* ignored (ABI 3: the encode kernel needs no scratch) */
+    uint64_t workspace_bytes;            /* ignored */
+    uint64_t out_cap;                    /* ignored (ABI 2 used it for the wire-tile kernel, since removed) */
 } hyobfs_gecko_batch;
 
 /* 0: kept for callers of ABI 1 (the wave-group kernel needs no workspace). */
 uint64_t hyobfs_gecko_workspace_size(uint64_t n);
-/* Scratch of this batch: 16 + 4 x ceil(out_cap / 16 KiB) bytes (0 without out_cap;
-   unused unless the wire-tile kernel is asked for).  After such a call, the 32-bit
-   word at offset 8 of a caller's workspace is 0 when the wire-tile kernel ran and 1
-   when the frames' placement sent the batch to the wave-group kernel (tests use it). */
-uint64_t hyobfs_gecko_workspace_bytes(const hyobfs_gecko_batch* b);
 /* A fresh 256-bit pad key and 96-bit nonce from the OS (getrandom, the source of
    crypto/rand).  Returns HYOBFS_OK or HYOBFS_ERR_IO. */
 int hyobfs_gecko_random_pad_key(uint8_t key[32], uint8_t nonce[12]);
@@ -142,8 +130,8 @@ int hyobfs_gecko_random_pad_key(uint8_t key[32], uint8_t nonce[12]);
  * Asynchronous on `stream` (NULL = null stream).  A frame the reference could
  * not have produced (total chunks outside [2, 8], chunk index >= total, or a
  * datagram longer than HYOBFS_GECKO_BUFFER_SIZE) is skipped on the device: its
- * output bytes are left untouched.  HYOBFS_ERR_INVALID for a missing pointer,
- * an all-zero pad_key or a workspace shorter than hyobfs_gecko_workspace_size(n).
+ * output bytes are left untouched.  HYOBFS_ERR_INVALID for a missing pointer
+ * or an all-zero pad_key.
  */
 int hyobfs_gecko_encode_batch(hyobfs_salamander* ctx, const hyobfs_gecko_batch* b, void* stream);
 

@@ -37,22 +37,18 @@ out = torch.empty(total + 16, dtype=torch.uint8, device=dev)
 dfr = torch.from_numpy(fr.view(np.uint8)).to(dev)
 doff = torch.from_numpy(off.view(np.uint8)).to(dev)
 alg = M * L + total
-modes = os.environ.get("AB_GK_MODES", "tile,wave").split(",")
-ws = torch.empty(max(16, gecko.workspace_bytes(out.numel())), dtype=torch.uint8, device=dev)
+modes = ["wave"]
 obs = {}
 for name, path in libs:
     for m in modes:
         o = hysteria_amd.SalamanderObfuscator(b"average_password", 0, lib_path=path)
-        if m == "tile":
-            o.set_kernel("stream")   # the wire-tile kernel is opt-in
         obs[f"{name}/{m}"] = o
 libs = [(f"{name}/{m}", path) for name, path in libs for m in modes]
 
 
 def run(name):
-    cap = out.numel() if name.endswith("/tile") else 0
     gecko.encode_batch(obs[name], msg=msg, frames=dfr, salts=salts, pad_key=bytes(range(32)), pad_nonce=bytes(12),
-                       out=out, out_off=doff, n=nf, out_cap=cap, workspace=ws, workspace_bytes=ws.numel())
+                       out=out, out_off=doff, n=nf)
 
 
 ref = None

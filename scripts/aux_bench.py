@@ -48,11 +48,10 @@ hysteria_amd.synth_stream(msg, M * L, 1, 0)
 salts = torch.empty(nf, dtype=torch.int64, device=dev)
 hysteria_amd.synth_u64(salts, nf, 2, 0)
 out = torch.empty(total + 16, dtype=torch.uint8, device=dev)
-ws = torch.empty(max(16, gecko.workspace_bytes(out.numel())), dtype=torch.uint8, device=dev)   # wire tiles
 o = hysteria_amd.SalamanderObfuscator(b"average_password", 0)
 dfr, doff = d(fr), d(off)
 ms = timed(lambda: gecko.encode_batch(o, msg=msg, frames=dfr, salts=salts, pad_key=bytes(range(1, 33)), pad_nonce=bytes(12), out=out, out_off=doff,
-                                      workspace=ws, n=nf))
+                                      n=nf))
 alg = M * L + total   # chunk bytes read + wire bytes written (pad generated on device)
 res["gecko_encode"] = {"messages": M, "msg_len": L, "frames": nf, "wire_bytes": total, "ms": round(ms, 4),
                        "frames_per_s": round(nf / ms * 1e3), "alg_GBs": round(alg / ms / 1e6, 1),

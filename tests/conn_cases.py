@@ -10,7 +10,7 @@ import socket
 
 import numpy as np
 
-from hysteria_amd.conn import SalamanderPacketConn
+from hysteria_amd.conn import SalamanderPacketConn, _sockaddr
 from hysteria_amd.salamander import SalamanderObfuscator
 from oracle import salamander_ref as ref
 
@@ -343,9 +343,45 @@ def run_lifecycle_scenarios(device: int = 0, n: int = 200, max_batch: int = 64, 
         wire, _ = raw.recvfrom(4096)
         assert ref.deobfuscate(PSK, wire) == b"after"
         cc.close()
+
+        # 4. free without close (a Go finalizer on a dropped connection): the
+        # connection owns the descriptor it was given, so free closes it -- and a
+        # coalescing one sends what write_to accepted before the socket goes
+        _free_unclosed_closes_fd(oa, r_addr, raw, max_batch)
     finally:
         raw.close()
         oa.close()
+
+
+def _free_unclosed_closes_fd(oa, r_addr, raw, max_batch):
+    """hyobfs_conn_wrap on a dup'd descriptor, hyobfs_conn_free with no
+    hyobfs_conn_close first (include/hyobfs_conn.h): the fd leaves the process's
+    descriptor table (fstat fails with EBADF), the caller's own socket is untouched,
+    and the coalescer's accepted datagrams are on the wire."""
+    import ctypes
+    import os
+    lib = oa._lib
+    for coalescing in (False, True):
+        s = _udp()
+        fd = os.dup(s.fileno())
+        h = ctypes.c_void_p()
+        assert lib.hyobfs_conn_wrap(fd, oa._h, max_batch, ctypes.byref(h)) == 0
+        if coalescing:
+            assert lib.hyobfs_conn_set_coalescing(h, max_batch, 100000) == 0
+            sa = _sockaddr(r_addr, socket.AF_INET)
+            assert lib.hyobfs_conn_write_to(h, b"freed but sent", 14, sa, len(sa)) == 14
+        os.fstat(fd)                      # open while wrapped
+        lib.hyobfs_conn_free(h)
+        try:
+            os.fstat(fd)
+            raise AssertionError(f"fd {fd} still open after hyobfs_conn_free (coalescing={coalescing})")
+        except OSError as e:
+            assert e.errno == errno.EBADF, e
+        os.fstat(s.fileno())              # the caller's socket is its own
+        if coalescing:
+            wire, _ = raw.recvfrom(4096)
+            assert ref.deobfuscate(PSK, wire) == b"freed but sent"
+        s.close()
 
 
 def run_deadline_scenarios(device: int = 0, max_batch: int = 16):

@@ -203,6 +203,11 @@ inline uint8_t* hyemu_dyn_lds() { return hyemu::g_ctx.dyn.get(); }
 inline hipError_t hipGetLastError() { return hipSuccess; }
 inline const char* hipGetErrorString(hipError_t) { return "emulated"; }
 inline hipError_t hipGetDeviceCount(int* n) { *n = 1; return hipSuccess; }
+inline hipError_t hipDeviceGetPCIBusId(char* buf, int len, int dev) {
+    if (dev != 0 || len < 13) return hipErrorInvalidValue;
+    std::snprintf(buf, (size_t)len, "0000:00:00.0");   // the one emulated device
+    return hipSuccess;
+}
 inline hipError_t hipGetDevice(int* d) { *d = 0; return hipSuccess; }
 inline hipError_t hipSetDevice(int d) { return d == 0 ? hipSuccess : hipErrorInvalidValue; }
 inline hipError_t hipGetDeviceProperties(hipDeviceProp_t* p, int) {

@@ -15,7 +15,7 @@ from oracle import salamander_ref as ref  # noqa: E402
 
 
 def run(obf, psk, lens, in_off, inp, salts, out_cap, out_stride=0, pkt_cap=0, in_stride=0, len_uniform=0,
-        contiguous=False, expect_kernel=None):
+        contiguous=False, expect_kernel=None, expect_ws=None):
     n = len(lens) if lens is not None else len(salts)
     co = ref.COracle()
     exp, eoff, elen, etot = co.batch(obf, psk, n, inp, in_off=in_off, in_stride=in_stride, in_len=lens,
@@ -35,6 +35,11 @@ def run(obf, psk, lens, in_off, inp, salts, out_cap, out_stride=0, pkt_cap=0, in
                                **({"salts": p(salts)} if obf else {}))
         want_k = os.environ.get("HYOBFS_KERNEL") == "wave" and "wave" or expect_kernel
         assert got_k == want_k, ("kernel", got_k, want_k)
+    if expect_ws is not None:   # hyobfs_batch_workspace_bytes, then a caller workspace of exactly that size
+        need = SalamanderObfuscator.workspace_bytes(inp=p(inp), n=n, **{k: v for k, v in kw.items() if k != "stream"})
+        assert need == expect_ws, ("workspace_bytes", need, expect_ws)
+        ws = np.zeros(need, np.uint8)   # ASan: a scratch overrun is a heap-buffer-overflow
+        kw.update(workspace=p(ws), workspace_bytes=need)
     if obf:
         o.obfuscate_batch(p(inp), n, salts=p(salts), **kw)
     else:
@@ -90,13 +95,16 @@ def case_packed_cap(seed, n, maxlen, obf, cap_pct, psk_len):
     run(obf, psk, lens, in_off, inp, salts, max(16, full * cap_pct // 100))
 
 
-def case_contig(seed, n, dist, obf, cap_pct, psk_len, pkt_cap=0, misalign=0):
-    """Contiguous packed input (in_off NULL, in_stride 0: datagram i right after
-    datagram i-1) into packed output: the stream kernel (salamander_stream.h).  dist 0:
-    the bimodal 64/1350 mix; 1: 0..2100 B; 2: 0..40 B (many datagrams per tile, several
-    per chunk: multi-pass tiles); 3: 1000..5000 B; 4: bimodal with zero-length ones.
-    out_cap cut to cap_pct % of the full size, pkt_cap drops, deobfuscate of real wire
-    (8-byte wire datagrams dropped), misalign = input not 16-byte aligned (the fallback)."""
+def case_contig(seed, n, dist, obf, cap_pct, psk_len, pkt_cap=0, misalign=0, out_stride=0):
+    """Contiguous input (in_off NULL, in_stride 0: datagram i right after datagram
+    i-1) into packed output (out_stride 0: the wave kernel scans the lengths itself;
+    with HYOBFS_PACKED_RUN_LOG2 < 6 a prepass writes the input offsets) or into slots
+    of out_stride bytes (the prepass's offsets, then the wave kernel).  dist 0: the
+    bimodal 64/1350 mix; 1: 0..2100 B; 2: 0..40 B (several datagrams per chunk);
+    3: 1000..5000 B; 4: bimodal with zero-length ones.  out_cap cut to cap_pct % of
+    the full size, pkt_cap drops, deobfuscate of real wire (8-byte wire datagrams
+    dropped), misalign = input not 16-byte aligned.  The call gets a caller workspace
+    of exactly hyobfs_batch_workspace_bytes, whose value is checked."""
     rng = np.random.default_rng(seed)
     psk = bytes((11 * i + 5) & 0xFF for i in range(psk_len))
     if dist == 0:
@@ -131,10 +139,11 @@ def case_contig(seed, n, dist, obf, cap_pct, psk_len, pkt_cap=0, misalign=0):
         # the wire is contiguous: datagrams back to back, as their out_off say
         assert np.array_equal(woff[1:], np.cumsum(wlen[:-1], dtype=np.uint64))
         inp, in_off, lens, total = winp, woff, np.ascontiguousarray(wlen, np.uint32), wl
-    full = total + (8 * n if obf else 0)
-    want = "stream" if os.environ.get("HYOBFS_KERNEL") == "stream" and not misalign else "wave"
+    full = n * out_stride if out_stride else total + (8 * n if obf else 0)
+    tsums = ((n + 255) // 256 + 1) * 8
+    prepass = out_stride or os.environ.get("HYOBFS_PACKED_RUN_LOG2", "6") != "6"
     run(obf, psk, lens, in_off, inp, salts, max(16, full * cap_pct // 100), pkt_cap=pkt_cap, contiguous=True,
-        expect_kernel=want)
+        out_stride=out_stride, expect_kernel="wave", expect_ws=2 * tsums + (8 * n if prepass else 0))
 
 
 def case_bimodal(n, obf):
@@ -234,7 +243,7 @@ def case_host(n, L, chunk, obf):
         assert out[i * out_stride:i * out_stride + len(exp)].tobytes() == exp, i
 
 
-def case_gecko(n_msgs, seed, layout=0, tiles=1):
+def case_gecko(n_msgs, seed, layout=0):
     """Gecko frames: one device encode pass vs oracle/gecko_ref, then deobfuscate + parse.
     layout 0: packed wire order (the aligned sweep); 1: ascending with gaps between
     frames (aligned sweep, gap bytes untouched); 2: frames placed in shuffled order
@@ -272,19 +281,10 @@ def case_gecko(n_msgs, seed, layout=0, tiles=1):
     salts = ref.splitmix64_array(5, 0, nf)
     out = np.full(total + 64, 0xA5, np.uint8)
     o = SalamanderObfuscator(psk, 0)
-    if tiles:
-        o.set_kernel("stream")   # the wire-tile kernel is opt-in
     p = lambda a: a.ctypes.data  # noqa: E731
     key, nonce = bytes(range(3, 35)), bytes(range(40, 52))
-    # out_cap given: frames in order run the wire-tile kernel (layouts 0, 1, 3), shuffled
-    # ones (layout 2) the wave-group kernel; tiles=0 runs the wave-group kernel only
-    out_cap = total + 64 if tiles else 0
-    ws = np.full(max(gecko.workspace_bytes(out_cap), 16), 0xEE, np.uint8)
     gecko.encode_batch(o, msg=p(msg), frames=p(fr), salts=p(salts), pad_key=key, pad_nonce=nonce, out=p(out),
-                       out_off=p(off), n=nf, stream=0, out_cap=out_cap, workspace=p(ws),
-                       workspace_bytes=gecko.workspace_bytes(out_cap))
-    if tiles:   # which kernel ran: the scratch's word at +8 is 0 when the wire tiles took the batch
-        assert int(ws[8:12].view(np.uint32)[0]) == (1 if layout == 2 else 0), ("tiled", layout)
+                       out_off=p(off), n=nf, stream=0)
     exp = gref.encode_wire(psk, msg.tobytes(), fr.tolist(), salts, key, nonce, off)
     assert out[total:].tobytes() == b"\xa5" * 64
     written = np.zeros(total + 64, bool)

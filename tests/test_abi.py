@@ -26,7 +26,7 @@ def test_library_exports_every_header_symbol():
 
 def test_abi_basics():
     lib = _lib.load()
-    assert lib.hyobfs_abi_version() == _lib.ABI_VERSION == 2
+    assert lib.hyobfs_abi_version() == _lib.ABI_VERSION == 3
     assert _lib.status_string(_lib.HYOBFS_ERR_PSK_TOO_SHORT) == "PSK must be at least 4 bytes"
     assert _lib.status_string(_lib.HYOBFS_ERR_CLOSED) == "use of closed connection"
     assert lib.hyobfs_batch_workspace_size(0) == 8
@@ -101,7 +101,7 @@ def test_header_abi_version_matches_bindings():
     assert int(re.search(r"#define HYOBFS_ERR_CLOSED \((-\d+)\)", text).group(1)) == _lib.HYOBFS_ERR_CLOSED
     from hysteria_amd.salamander import SalamanderObfuscator
     kernels = {m.group(1).lower(): int(m.group(2)) for m in re.finditer(r"HYOBFS_KERNEL_(\w+) = (\d+)", text)}
-    assert kernels == SalamanderObfuscator.KERNELS   # auto, wave, tile, stream
+    assert kernels == SalamanderObfuscator.KERNELS   # auto, wave, tile
 
 
 def test_load_refuses_other_abi_version(tmp_path):

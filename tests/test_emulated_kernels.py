@@ -46,7 +46,7 @@ SPECS = {
                                 "HYOBFS_KERNEL": "wave"}),
     "test_emulated_kernel_vs_oracle": lambda p: (p["which"], p["args"], {"HYEMU_CUS": p["cus"]}),
     "test_emulated_split_launches": lambda p: (p["which"], p["args"], dict(p["env"])),
-    "test_emulated_stream_kernel": lambda p: ("contig", p["args"], {"HYEMU_CUS": "2", "HYOBFS_KERNEL": "stream"}),
+    "test_emulated_contiguous_input_slotted": lambda p: ("contig", p["args"], {"HYEMU_CUS": "2"}),
     "test_emulated_contiguous_input_auto": lambda p: ("contig", p["args"], {"HYEMU_CUS": "2"}),
     "test_emulated_contiguous_input_prepass_offsets": lambda p: ("contig", p["args"], {
         "HYEMU_CUS": "2", "HYOBFS_PACKED_RUN_LOG2": "3"}),
@@ -116,9 +116,7 @@ CASES = [
     ("gecko", "60 8 1", "2"),            # ... ascending frames with gaps: gap bytes untouched
     ("gecko", "60 9 2", "2"),            # ... shuffled placement: the per-frame path
     ("gecko", "70 10 3", "2"),           # ... tiny frames, several per 16-byte chunk
-    ("gecko", "300 11 0", "2"),          # ... the wire-tile kernel over several tiles
-    ("gecko", "40 7 0 0", "2"),          # ... no out_cap: the wave-group kernel alone
-    ("gecko", "60 8 1 0", "2"),
+    ("gecko", "300 11 0", "2"),          # ... many groups
     ("punch", "300 5 3", "2"),           # realm punch matcher (realm.hip)
     ("quic", "2", "2"),                  # QUIC Initial unprotect + ReadCryptoPayload kernels (quic.hip)
 ]
@@ -150,14 +148,13 @@ PACKED_CASES = [
 ]
 
 
-# Contiguous packed input (in_off NULL, in_stride 0) into packed output
-# (tests/emu/run_case.py case_contig: seed n dist obf cap% psk_len [pkt_cap misalign]):
-# AUTO = the wave kernel taking its input offsets from the scan of the lengths;
-# HYOBFS_KERNEL=stream the stream kernel (salamander_stream.h); wave runs of 8 the
-# stream prepass's input offsets.  Bimodal, 0..2100 B, tiny (multi-pass tiles, several
-# datagrams per chunk), 1-5 KB, zero-length datagrams; out_cap cuts, pkt_cap drops,
-# real wire with 8-byte datagrams, PSKs across salt words and the two-block case, a
-# misaligned input.
+# Contiguous input (in_off NULL, in_stride 0; tests/emu/run_case.py case_contig:
+# seed n dist obf cap% psk_len [pkt_cap misalign out_stride]).  Packed output under
+# AUTO: the wave kernel taking its input offsets from the scan of the lengths; packed
+# runs of 8 or slotted output: the prepass's input offsets (in_offsets_kernel), then
+# the wave kernel.  Bimodal, 0..2100 B, tiny (several datagrams per chunk), 1-5 KB,
+# zero-length datagrams; out_cap cuts, pkt_cap drops, real wire with 8-byte
+# datagrams, PSKs across salt words and the two-block case, a misaligned input.
 CONTIG_CASES = [
     "1 3000 0 1 100 16", "2 3000 0 0 100 16", "3 2000 1 1 100 16", "4 2000 1 0 100 33", "5 3000 2 1 100 16",
     "6 3000 2 0 100 121", "7 300 3 1 100 16", "8 300 3 0 100 4", "9 3000 4 1 100 16", "10 3000 4 0 100 16",
@@ -167,16 +164,6 @@ CONTIG_CASES = [
 
 
 @pytest.mark.parametrize("args", CONTIG_CASES)
-def test_emulated_stream_kernel(emu_lib, args):
-    _run(emu_lib, "contig", args, {"HYEMU_CUS": "2", "HYOBFS_KERNEL": "stream"})
-
-
-# AUTO: the cases whose layout differs for the wave kernel's length scan (bimodal, ragged,
-# tiny, zero lengths, cuts, drops, two-block PSK, misaligned input)
-CONTIG_AUTO = [CONTIG_CASES[i] for i in (0, 1, 2, 4, 8, 10, 11, 13, 14)]
-
-
-@pytest.mark.parametrize("args", CONTIG_AUTO)
 def test_emulated_contiguous_input_auto(emu_lib, args):
     _run(emu_lib, "contig", args, {"HYEMU_CUS": "2"})
 
@@ -184,6 +171,24 @@ def test_emulated_contiguous_input_auto(emu_lib, args):
 @pytest.mark.parametrize("args", [CONTIG_CASES[i] for i in (1, 2, 10)])
 def test_emulated_contiguous_input_prepass_offsets(emu_lib, args):
     _run(emu_lib, "contig", args, {"HYEMU_CUS": "2", "HYOBFS_PACKED_RUN_LOG2": "3"})
+
+
+# Contiguous input into SLOTS (out_stride > 0): the prepass writes the input offsets
+# into the caller's workspace (8 B per datagram after the two sum arrays), the wave
+# kernel reads them.  Bimodal into 1358/1350-byte slots (everything fits), 0..2100 B
+# into 1200-byte slots (the slot drops the long ones), out_cap cutting the slots,
+# pkt_cap drops, a misaligned input, a two-block PSK, tiny datagrams in 48-byte slots.
+CONTIG_SLOTTED = [
+    "21 3000 0 1 100 16 0 0 1358", "22 3000 0 0 100 16 0 0 1350", "23 2000 1 1 100 16 0 0 1200",
+    "24 2000 1 0 100 33 0 0 1200", "25 2000 1 1 60 16 0 0 2112", "26 2000 1 0 70 127 0 0 2104",
+    "27 2000 1 1 100 16 900 0 1208", "28 2000 1 0 100 16 700 1 2104", "29 3000 2 1 100 121 0 0 48",
+    "30 3000 4 0 100 16 0 0 1350",
+]
+
+
+@pytest.mark.parametrize("args", CONTIG_SLOTTED)
+def test_emulated_contiguous_input_slotted(emu_lib, args):
+    _run(emu_lib, "contig", args, {"HYEMU_CUS": "2"})
 
 
 @pytest.mark.parametrize("which,args", PACKED_CASES)

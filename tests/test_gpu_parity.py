@@ -380,20 +380,15 @@ def test_config3_bimodal_4M_digest(obfs, gpu, golden):
     assert h.hexdigest() == d["obf_sha256"]
 
 
-# ------------------------------------------- contiguous input: wave scan / stream kernel
-@pytest.fixture(params=["auto", "stream", "wave"])
+# ------------------------------------------- contiguous input: the wave kernel's length scan
+@pytest.fixture(params=["auto", "wave"])
 def contig_obfs(gpu, request):
-    """auto and wave: the wave kernel scanning the input lengths with the widths;
-    stream: the stream kernel (salamander_stream.h)."""
+    """auto and wave: the wave kernel scanning the input lengths with the widths."""
     import hysteria_amd
     o = hysteria_amd.SalamanderObfuscator(PSK, 0)
     o.set_kernel(request.param)
     yield o
     o.close()
-
-
-def _stream_expected(obfs):
-    return "stream" if obfs.kernel == "stream" else "wave"
 
 
 def test_contiguous_bimodal_64k_vs_oracle_and_digest(contig_obfs, gpu, coracle, golden):
@@ -412,7 +407,7 @@ def test_contiguous_bimodal_64k_vs_oracle_and_digest(contig_obfs, gpu, coracle, 
     out_len = torch.empty(n, dtype=torch.int32, device=gpu)
     total = torch.zeros(1, dtype=torch.int64, device=gpu)
     kw = dict(in_len=lens, out=out, out_cap=cap, out_off=out_off, out_len=out_len, out_total=total)
-    assert obfs.batch_kernel(True, inp=inp, n=n, salts=salts, **kw) == _stream_expected(obfs)
+    assert obfs.batch_kernel(True, inp=inp, n=n, salts=salts, **kw) == "wave"
     obfs.obfuscate_batch(inp, n, salts=salts, **kw)
     got = _host(out)
     assert hashlib.sha256(got[:cap].tobytes()).hexdigest() == d["obf_sha256"]
@@ -426,7 +421,7 @@ def test_contiguous_bimodal_64k_vs_oracle_and_digest(contig_obfs, gpu, coracle, 
     assert int(_host(total)[0]) == etot
     back = torch.full((total_in + 64,), 0x5A, dtype=torch.uint8, device=gpu)
     kw = dict(in_len=out_len, out=back, out_cap=total_in, out_total=total)
-    assert obfs.batch_kernel(False, inp=out, n=n, **kw) == _stream_expected(obfs)
+    assert obfs.batch_kernel(False, inp=out, n=n, **kw) == "wave"
     obfs.deobfuscate_batch(out, n, **kw)
     hb = _host(back)
     assert np.array_equal(hb[:total_in], _host(inp)[:total_in])
@@ -458,25 +453,36 @@ def test_contiguous_config3_4M_digest_and_roundtrip(contig_obfs, gpu, golden):
     assert torch.equal(back[:total_in], inp[:total_in])
 
 
-# seed, n, length distribution, obfuscate, out_cap %, PSK length, pkt_cap, input misalignment
-# (dist 0 bimodal, 1: 0..2100 B, 2: 0..40 B (multi-pass tiles), 3: 1..5 KB, 4: bimodal + zeros)
-CONTIG_GPU = [(1, 20000, 0, 1, 100, 16, 0, 0), (2, 20000, 0, 0, 100, 16, 0, 0), (3, 8000, 1, 1, 100, 33, 0, 0),
-              (4, 8000, 1, 0, 100, 121, 0, 0), (5, 20000, 2, 1, 100, 16, 0, 0), (6, 20000, 2, 0, 100, 4, 0, 0),
-              (7, 2000, 3, 1, 100, 127, 0, 0), (8, 2000, 3, 0, 100, 16, 0, 0), (9, 20000, 4, 1, 100, 16, 0, 0),
-              (10, 20000, 4, 0, 100, 16, 0, 0), (11, 8000, 1, 1, 60, 16, 0, 0), (12, 8000, 1, 0, 70, 16, 0, 0),
-              (13, 8000, 1, 1, 100, 16, 1000, 0), (14, 8000, 1, 0, 100, 16, 900, 0), (15, 20000, 0, 1, 100, 16, 0, 1),
-              (16, 20000, 0, 0, 100, 16, 0, 3)]
+# seed, n, length distribution, obfuscate, out_cap %, PSK length, pkt_cap, input misalignment,
+# out_stride (0: packed output)
+# (dist 0 bimodal, 1: 0..2100 B, 2: 0..40 B (several per chunk), 3: 1..5 KB, 4: bimodal + zeros)
+CONTIG_GPU = [(1, 20000, 0, 1, 100, 16, 0, 0, 0), (2, 20000, 0, 0, 100, 16, 0, 0, 0),
+              (3, 8000, 1, 1, 100, 33, 0, 0, 0), (4, 8000, 1, 0, 100, 121, 0, 0, 0),
+              (5, 20000, 2, 1, 100, 16, 0, 0, 0), (6, 20000, 2, 0, 100, 4, 0, 0, 0),
+              (7, 2000, 3, 1, 100, 127, 0, 0, 0), (8, 2000, 3, 0, 100, 16, 0, 0, 0),
+              (9, 20000, 4, 1, 100, 16, 0, 0, 0), (10, 20000, 4, 0, 100, 16, 0, 0, 0),
+              (11, 8000, 1, 1, 60, 16, 0, 0, 0), (12, 8000, 1, 0, 70, 16, 0, 0, 0),
+              (13, 8000, 1, 1, 100, 16, 1000, 0, 0), (14, 8000, 1, 0, 100, 16, 900, 0, 0),
+              (15, 20000, 0, 1, 100, 16, 0, 1, 0), (16, 20000, 0, 0, 100, 16, 0, 3, 0),
+              # slotted output: the prepass writes the input offsets into the workspace
+              (21, 20000, 0, 1, 100, 16, 0, 0, 1358), (22, 20000, 0, 0, 100, 16, 0, 0, 1350),
+              (23, 8000, 1, 1, 100, 16, 0, 0, 1200), (24, 8000, 1, 0, 100, 33, 0, 0, 1200),
+              (25, 8000, 1, 1, 60, 16, 0, 0, 2112), (26, 8000, 1, 0, 70, 127, 0, 0, 2104),
+              (27, 8000, 1, 1, 100, 16, 900, 0, 1208), (28, 8000, 1, 0, 100, 16, 700, 1, 2104),
+              (29, 20000, 2, 1, 100, 121, 0, 0, 48), (30, 20000, 4, 0, 100, 16, 0, 0, 1350)]
 
 
 @pytest.mark.parametrize("case", CONTIG_GPU)
 def test_contiguous_input_grid_vs_oracle(contig_obfs, gpu, coracle, case):
     """The contiguous layout's edge cases under each kernel choice, byte for byte against
-    the C oracle, sentinel bytes past the output: tiles with more than 64 datagrams and several per 16-byte chunk,
+    the C oracle, sentinel bytes past the output: several datagrams per 16-byte chunk,
     zero-length datagrams, out_cap cuts (the tail), pkt_cap drops (holes in the input),
     real wire with 8-byte datagrams, PSKs across salt words and two blocks, misaligned
-    input (the offsets + wave kernel fallback)."""
+    input; packed output and slotted output (out_stride > 0: the prepass's input
+    offsets).  The call gets a caller workspace of exactly hyobfs_batch_workspace_bytes
+    (checked against the documented sizing) with sentinel bytes behind it."""
     import torch
-    seed, n, dist, obf, cap_pct, psk_len, pkt_cap, mis = case
+    seed, n, dist, obf, cap_pct, psk_len, pkt_cap, mis, stride = case
     rng = np.random.default_rng(seed)
     psk = bytes((11 * i + 5) & 0xFF for i in range(psk_len))
     lens = {0: lambda: ref.bimodal_lengths(3, seed, n), 1: lambda: rng.integers(0, 2100, n),
@@ -491,10 +497,11 @@ def test_contiguous_input_grid_vs_oracle(contig_obfs, gpu, coracle, case):
         wire, woff, wlen, _ = coracle.batch(True, psk, n, inp, in_off=in_off, in_len=lens, salts=salts,
                                             out_cap=total + 8 * n)
         inp, in_off, lens, total = np.concatenate([wire, np.zeros(32, np.uint8)]), woff, wlen.copy(), int(wlen.sum())
-    full = total + (8 * n if obf else 0)
+    full = n * stride if stride else total + (8 * n if obf else 0)
     cap = max(16, full * cap_pct // 100)
     exp, eoff, elen, etot = coracle.batch(bool(obf), psk, n, inp, in_off=in_off, in_len=lens,
-                                          salts=salts if obf else None, out_cap=cap, pkt_cap=pkt_cap)
+                                          salts=salts if obf else None, out_cap=cap, pkt_cap=pkt_cap,
+                                          out_stride=stride)
     d_in = torch.zeros(len(inp) + 16, dtype=torch.uint8, device=gpu)
     d_in[mis:mis + len(inp)] = torch.from_numpy(inp).to(gpu)
     src = d_in[mis:]
@@ -503,17 +510,20 @@ def test_contiguous_input_grid_vs_oracle(contig_obfs, gpu, coracle, case):
     out_len = torch.zeros(n, dtype=torch.int32, device=gpu)
     tot = torch.zeros(1, dtype=torch.int64, device=gpu)
     kw = dict(in_len=_u32(lens, gpu), out=out, out_cap=cap, pkt_cap=pkt_cap, out_off=out_off, out_len=out_len,
-              out_total=tot)
+              out_total=tot, out_stride=stride)
     if obf:
         kw["salts"] = _u64(salts, gpu)
     import hysteria_amd
-    kern = contig_obfs.kernel
-    want = "stream" if kern == "stream" and not mis else "wave"
+    tsums = ((n + 255) // 256 + 1) * 8
+    need = hysteria_amd.SalamanderObfuscator.workspace_bytes(inp=src, n=n, **kw)
+    assert need == 2 * tsums + (8 * n if stride else 0)
+    ws = torch.full((need + 64,), 0x3C, dtype=torch.uint8, device=gpu)
     with hysteria_amd.SalamanderObfuscator(psk, 0) as o:   # the case's PSK (the fixture's is average_password)
-        o.set_kernel(kern)
-        assert o.batch_kernel(bool(obf), inp=src, n=n, **kw) == want
-        (o.obfuscate_batch if obf else o.deobfuscate_batch)(inp=src, n=n, **kw)
+        o.set_kernel(contig_obfs.kernel)
+        assert o.batch_kernel(bool(obf), inp=src, n=n, **kw) == "wave"
+        (o.obfuscate_batch if obf else o.deobfuscate_batch)(inp=src, n=n, workspace=ws, workspace_bytes=need, **kw)
         got = _host(out)
+    assert (_host(ws)[need:] == 0x3C).all(), "wrote past the workspace"
     assert np.array_equal(_host(out_off).view(np.uint64), eoff)
     assert np.array_equal(_host(out_len).view(np.uint32), elen)
     assert int(_host(tot)[0]) == etot

@@ -18,7 +18,7 @@ import pytest
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "emu"))
 from emu_build import ensure_emu_lib  # noqa: E402
 
-from hysteria_amd.shard import byte_balanced_split, even_split, weak_shard
+from hysteria_amd.shard import byte_balanced_split, check_rank_devices, even_split, weak_shard
 from oracle import salamander_ref as ref
 
 PSK = b"average_password"
@@ -50,6 +50,20 @@ def test_byte_balanced_split_partitions_and_balances():
 
 def test_weak_shard():
     assert weak_shard(1 << 20, 3) == (3 << 20, 1 << 20)
+
+
+def test_check_rank_devices():
+    """bench.py's rank binding check: distinct cards pass; two ranks on one card are a
+    flagged rehearsal when the node has fewer cards than ranks, and an error when it
+    has a card per rank (a misconfigured LOCAL_RANK / HIP_VISIBLE_DEVICES)."""
+    ids = [f"0000:{0x11 + 16 * i:02x}:00.0" for i in range(8)]
+    assert check_rank_devices(ids, 8) is False
+    assert check_rank_devices(ids[:1], 1) is False
+    assert check_rank_devices([ids[0], ids[0]], 1) is True       # --gpus 2 on a one-card box
+    with pytest.raises(RuntimeError, match="share"):
+        check_rank_devices([ids[0], ids[1], ids[0], ids[3]], 8)
+    with pytest.raises(RuntimeError):
+        check_rank_devices([ids[0], ids[0]], 2)
 
 
 def _free_port():
