@@ -7,15 +7,19 @@
 // batch:
 //   * send: WriteTo reserves a slot in the filling batch (a short spin lock),
 //     copies the datagram and returns len(p).  A flusher thread seals the batch
-//     when it is full or max_wait_us after its first datagram, obfuscates it on
-//     the GPU (pinned staging, hyobfs_salamander_obfuscate_host) and sends it
-//     with sendmmsg, while the next batch fills.  Like a UDP sendto, the call
+//     when it is full or max_wait_us after its first datagram and launches its
+//     obfuscation on the GPU, which reads and writes the batch in place (mapped
+//     pinned memory, gpu_queue_submit); while that kernel runs the thread sends
+//     the PREVIOUS batch with sendmmsg, and the next batch fills.  Three send
+//     batches rotate: filling, on the GPU, on the wire.  Like a UDP sendto, the call
 //     returns once the datagram is queued.  A later send failure is counted and
 //     its errno is returned by the NEXT WriteTo on the connection (-1, that
 //     datagram not accepted): the reference returns it to the caller whose
 //     datagram failed (conn.go:93-98), which a queued send cannot do.
 //   * receive: a reader thread receives up to max_batch datagrams with
-//     recvmmsg, deobfuscates them in one GPU batch and queues the batch;
+//     recvmmsg and launches their deobfuscation as one GPU batch; while it runs
+//     the thread hands the previous batch to the queue and receives the next one
+//     (when the socket has nothing more, it finishes the batch on the GPU first);
 //     ReadFrom takes the next datagram from the queue.  Datagrams that do not
 //     deobfuscate are dropped and an empty datagram is a 0-byte read, as in
 //     ReadFrom (conn.go:77-86).  The socket's SO_RCVTIMEO bounds the wait (one
@@ -37,6 +41,7 @@
 
 #include <atomic>
 #include <chrono>
+#include <cstdlib>
 #include <condition_variable>
 #include <deque>
 #include <mutex>
@@ -75,6 +80,22 @@ struct Pinned {   // device-mapped pinned slots of kBuf bytes
     }
 };
 
+// HYOBFS_COALESCE_OVERLAP=0: no overlap (seal, GPU, send one batch at a time);
+// HYOBFS_COALESCE_ZEROCOPY=0: the GPU step through hyobfs_salamander_*_host (staged
+// copies, synchronous) instead of in place.  Both 1 by default; A/B knobs, read once.
+static bool env_flag(const char* name, bool dflt) {
+    const char* e = std::getenv(name);
+    return e ? std::atoi(e) != 0 : dflt;
+}
+static bool overlap_on() {
+    static const bool v = env_flag("HYOBFS_COALESCE_OVERLAP", true);
+    return v;
+}
+static bool zerocopy_on() {
+    static const bool v = env_flag("HYOBFS_COALESCE_ZEROCOPY", true);
+    return v;
+}
+
 struct Batch {
     Pinned b;
     std::vector<sockaddr_storage> addr;
@@ -86,6 +107,7 @@ struct Batch {
     bool sealed = false;
     Clock::time_point first{};
     std::atomic<uint32_t> committed{0};
+    bool gpu_ok = false;   // its GPU step was launched (or done) without error
     // receive side (k / next under rx_mu)
     uint32_t k = 0, next = 0;
     std::atomic<uint32_t> done{0};
@@ -139,8 +161,11 @@ struct Coalescer {
     uint32_t max_batch = 0;
     std::chrono::microseconds max_wait{0};
     std::atomic<bool> stop{false};
-    // send
-    Batch tx[2];
+    GpuQueue* gq_tx = nullptr;           // the send side's stream (gpu_queue_*)
+    GpuQueue* gq_rx = nullptr;
+    // send: batches rotate filling -> on the GPU -> on the wire
+    static constexpr int kTx = 3;
+    Batch tx[kTx];
     int cur = 0;                         // filling batch, under spin
     Spin spin;
     std::mutex tx_mu;                    // waits: flusher for datagrams, writers for space
@@ -149,7 +174,8 @@ struct Coalescer {
     std::atomic<int> tx_err_pending{0};  // errno of the first failed send not yet reported
     std::thread flusher;
     // receive
-    Batch rx[3];
+    static constexpr int kRx = 4;
+    Batch rx[kRx];
     std::mutex rx_mu;
     std::condition_variable cv_ready, cv_free;
     std::deque<int> ready, freelist;
@@ -162,11 +188,19 @@ struct Coalescer {
 
     bool has_space() const { return !tx[cur].sealed && tx[cur].count < max_batch; }
     void flush_loop();
-    void send_batch(Batch& b, uint32_t n);
+    void submit_tx(int i);
+    void finish_tx(int i);
     void read_loop();
+    void submit_rx(int i, uint32_t k);
+    void finish_rx(int i);
 };
 
-void Coalescer::send_batch(Batch& b, uint32_t n) {
+// The sealed batch i onto the GPU: salts, then one obfuscate launch in place (or,
+// HYOBFS_COALESCE_ZEROCOPY=0, the synchronous staged call).
+void Coalescer::submit_tx(int i) {
+    Batch& b = tx[i];
+    const uint32_t n = b.count;   // no writer changes a sealed batch's count
+    while (b.committed.load(std::memory_order_acquire) < n) std::this_thread::yield();
     hyobfs_salamander_next_salts(ctx, reinterpret_cast<uint8_t*>(b.b.salts), n);   // RandSrc, salamander.go:65
     hyobfs_batch d{};
     d.n = n;
@@ -178,46 +212,65 @@ void Coalescer::send_batch(Batch& b, uint32_t n) {
     d.out_stride = kBuf;   // len(writeBuf): Obfuscate needs len + 8 <= 2048, else an empty datagram
     d.out_cap = (uint64_t)n * kBuf;
     d.out_len = b.b.olen;
-    if (hyobfs_salamander_obfuscate_host(ctx, &d, 0) != HYOBFS_OK) {
+    b.gpu_ok = (zerocopy_on() ? gpu_queue_submit(gq_tx, &d, true, i) : hyobfs_salamander_obfuscate_host(ctx, &d, 0)) ==
+               HYOBFS_OK;
+}
+
+// Waits for batch i's kernel, sends it with sendmmsg and frees the batch for writers.
+void Coalescer::finish_tx(int i) {
+    Batch& b = tx[i];
+    const uint32_t n = b.count;
+    if (b.gpu_ok && zerocopy_on()) b.gpu_ok = gpu_queue_wait(gq_tx, i) == HYOBFS_OK;
+    if (!b.gpu_ok) {
         tx_errors += n;
         int z = 0;
         tx_err_pending.compare_exchange_strong(z, EIO);
-        sent += n;   // handled (lost): flush() must not wait for them
-        return;
-    }
-    for (uint32_t i = 0; i < n; ++i) {
-        b.iov[i].iov_base = b.b.out + (size_t)i * kBuf;
-        b.iov[i].iov_len = b.b.olen[i];
-        memset(&b.msg[i], 0, sizeof(mmsghdr));
-        b.msg[i].msg_hdr.msg_iov = &b.iov[i];
-        b.msg[i].msg_hdr.msg_iovlen = 1;
-        b.msg[i].msg_hdr.msg_name = &b.addr[i];
-        b.msg[i].msg_hdr.msg_namelen = b.alen[i];
-    }
-    uint32_t done = 0;
-    while (done < n) {
-        const int r = sendmmsg(fd, b.msg.data() + done, n - done, 0);
-        if (r > 0) {
-            done += (uint32_t)r;
-            continue;
+    } else {
+        for (uint32_t j = 0; j < n; ++j) {
+            b.iov[j].iov_base = b.b.out + (size_t)j * kBuf;
+            b.iov[j].iov_len = b.b.olen[j];
+            memset(&b.msg[j], 0, sizeof(mmsghdr));
+            b.msg[j].msg_hdr.msg_iov = &b.iov[j];
+            b.msg[j].msg_hdr.msg_iovlen = 1;
+            b.msg[j].msg_hdr.msg_name = &b.addr[j];
+            b.msg[j].msg_hdr.msg_namelen = b.alen[j];
         }
-        if (r < 0 && errno == EINTR) continue;
-        if (r < 0 && (errno == EAGAIN || errno == ENOBUFS)) {   // socket buffer full: wait for room
-            pollfd pf{fd, POLLOUT, 0};
-            (void)poll(&pf, 1, 10);
-            continue;
+        uint32_t done = 0;
+        while (done < n) {
+            const int r = sendmmsg(fd, b.msg.data() + done, n - done, 0);
+            if (r > 0) {
+                done += (uint32_t)r;
+                continue;
+            }
+            if (r < 0 && errno == EINTR) continue;
+            if (r < 0 && (errno == EAGAIN || errno == ENOBUFS)) {   // socket buffer full: wait for room
+                pollfd pf{fd, POLLOUT, 0};
+                (void)poll(&pf, 1, 10);
+                continue;
+            }
+            ++tx_errors;   // this datagram cannot be sent (e.g. no route): skip it, report it to the next WriteTo
+            int z = 0;
+            tx_err_pending.compare_exchange_strong(z, errno ? errno : EIO);
+            ++done;
         }
-        ++tx_errors;   // this datagram cannot be sent (e.g. no route): skip it, report it to the next WriteTo
-        int z = 0;
-        tx_err_pending.compare_exchange_strong(z, errno ? errno : EIO);
-        ++done;
+        ++tx_batches;
     }
-    sent += n;
-    ++tx_batches;
+    sent += n;   // handled (sent or lost): flush() must not wait for them
+    spin.lock();
+    b.count = 0;
+    b.committed.store(0, std::memory_order_relaxed);
+    b.sealed = false;
+    spin.unlock();
+    {
+        std::lock_guard<std::mutex> lk(tx_mu);   // writers waiting for space re-check under tx_mu
+    }
+    cv_space.notify_all();
 }
 
 void Coalescer::flush_loop() {
+    int prev = -1;   // a batch whose kernel was launched and which is not sent yet
     for (;;) {
+        int sealed = -1;
         {
             std::unique_lock<std::mutex> lk(tx_mu);
             auto pending = [&] {
@@ -226,57 +279,107 @@ void Coalescer::flush_loop() {
                 spin.unlock();
                 return p;
             };
-            cv_flush.wait(lk, [&] { return stop.load() || pending(); });
-            if (!pending()) return;   // stopping, nothing left to send
-            spin.lock();
-            const Clock::time_point deadline = tx[cur].first + max_wait;
-            spin.unlock();
-            cv_flush.wait_until(lk, deadline, [&] {
+            auto due = [&] {
                 spin.lock();
                 const bool full = tx[cur].count >= max_batch;
                 spin.unlock();
                 return full || stop.load();
-            });
-            // seal the filling batch; writers move on to the other one (already sent)
-            spin.lock();
-            Batch& b = tx[cur];
-            b.sealed = true;
-            cur ^= 1;
-            spin.unlock();
+            };
+            if (prev < 0) {
+                cv_flush.wait(lk, [&] { return stop.load() || pending(); });
+                if (!pending()) return;   // stopping, nothing left to send
+            }
+            if (pending()) {
+                spin.lock();
+                const Clock::time_point deadline = tx[cur].first + max_wait;
+                spin.unlock();
+                // nothing on the GPU: wait for the batch to fill or its deadline; a batch on
+                // the GPU: seal this one only if it is due now, else send that one first
+                const bool go = prev < 0 ? (cv_flush.wait_until(lk, deadline, due), true)
+                                         : due() || Clock::now() >= deadline;
+                if (go) {   // seal the filling batch; writers move on to the next (already sent)
+                    spin.lock();
+                    tx[cur].sealed = true;
+                    sealed = cur;
+                    cur = (cur + 1) % kTx;
+                    spin.unlock();
+                }
+            }
         }
-        cv_space.notify_all();
-        Batch& b = tx[cur ^ 1];
-        const uint32_t n = b.count;   // no writer changes a sealed batch's count
-        while (b.committed.load(std::memory_order_acquire) < n) std::this_thread::yield();
-        send_batch(b, n);
-        spin.lock();
-        b.count = 0;
-        b.committed.store(0, std::memory_order_relaxed);
-        b.sealed = false;
-        spin.unlock();
-        {
-            std::lock_guard<std::mutex> lk(tx_mu);   // writers waiting for space re-check under tx_mu
+        if (sealed >= 0) {
+            cv_space.notify_all();
+            submit_tx(sealed);
         }
-        cv_space.notify_all();
+        if (prev >= 0) finish_tx(prev);
+        prev = sealed;
+        if (prev >= 0 && !overlap_on()) {
+            finish_tx(prev);
+            prev = -1;
+        }
     }
 }
 
+void Coalescer::submit_rx(int i, uint32_t k) {
+    Batch& b = rx[i];
+    for (uint32_t j = 0; j < k; ++j) {
+        b.b.len[j] = b.msg[j].msg_len;
+        b.alen[j] = b.msg[j].msg_hdr.msg_namelen;
+    }
+    hyobfs_batch d{};
+    d.n = (uint64_t)k;
+    d.in = b.b.in;
+    d.in_stride = kBuf;
+    d.in_len = b.b.len;
+    d.out = b.b.out;
+    d.out_stride = kBuf;
+    d.out_cap = (uint64_t)k * kBuf;
+    d.out_len = b.b.olen;
+    b.k = k;
+    b.gpu_ok = (zerocopy_on() ? gpu_queue_submit(gq_rx, &d, false, i) : hyobfs_salamander_deobfuscate_host(ctx, &d, 0)) ==
+               HYOBFS_OK;
+    received += (uint64_t)k;
+}
+
+// Waits for batch i's kernel and queues it for ReadFrom.
+void Coalescer::finish_rx(int i) {
+    Batch& b = rx[i];
+    if (b.gpu_ok && zerocopy_on()) b.gpu_ok = gpu_queue_wait(gq_rx, i) == HYOBFS_OK;
+    if (!b.gpu_ok)
+        for (uint32_t j = 0; j < b.k; ++j) b.b.olen[j] = 0;   // nothing deobfuscated: every datagram dropped
+    ++rx_batches;
+    {
+        std::lock_guard<std::mutex> lk(rx_mu);
+        b.next = 0;
+        b.done.store(0, std::memory_order_relaxed);
+        ready.push_back(i);
+    }
+    cv_ready.notify_all();
+}
+
 void Coalescer::read_loop() {
+    int prev = -1;   // a batch whose kernel was launched and which is not queued yet
     for (;;) {
         int bi;
         {
             std::unique_lock<std::mutex> lk(rx_mu);
             cv_free.wait(lk, [&] { return stop.load() || !freelist.empty(); });
-            if (stop) return;
+            if (stop) break;
             bi = freelist.front();
             freelist.pop_front();
         }
         Batch& b = rx[bi];
         int k = -1;
         while (!stop) {
+            // with a batch on the GPU only look: nothing waiting means queue that one first
             pollfd pf{fd, POLLIN, 0};
-            const int pr = poll(&pf, 1, 50);
-            if (pr <= 0) continue;   // timeout or EINTR: check stop, poll again
+            const int pr = poll(&pf, 1, prev >= 0 ? 0 : 50);
+            if (pr <= 0) {   // timeout or EINTR: check stop, poll again
+                if (prev >= 0) {
+                    finish_rx(prev);
+                    prev = -1;
+                }
+                continue;
+            }
             for (uint32_t i = 0; i < max_batch; ++i) {
                 b.iov[i].iov_base = b.b.in + (size_t)i * kBuf;
                 b.iov[i].iov_len = kBuf;
@@ -290,6 +393,10 @@ void Coalescer::read_loop() {
             if (k > 0) break;
             if (k < 0 && errno != EAGAIN && errno != EWOULDBLOCK && errno != EINTR) {
                 const int e = errno;
+                if (prev >= 0) {   // what was received before the error is delivered first
+                    finish_rx(prev);
+                    prev = -1;
+                }
                 std::unique_lock<std::mutex> lk(rx_mu);
                 // the socket is gone (closed under us): every later ReadFrom fails with
                 // it (Go: net.ErrClosed each time), the thread parks until stop instead
@@ -309,35 +416,20 @@ void Coalescer::read_loop() {
             std::lock_guard<std::mutex> lk(rx_mu);
             freelist.push_back(bi);
             cv_ready.notify_all();
-            if (stop) return;
+            if (stop) break;
             continue;
         }
-        for (int i = 0; i < k; ++i) {
-            b.b.len[i] = b.msg[i].msg_len;
-            b.alen[i] = b.msg[i].msg_hdr.msg_namelen;
+        submit_rx(bi, (uint32_t)k);
+        if (prev >= 0) finish_rx(prev);
+        prev = bi;
+        if (!overlap_on()) {
+            finish_rx(prev);
+            prev = -1;
         }
-        hyobfs_batch d{};
-        d.n = (uint64_t)k;
-        d.in = b.b.in;
-        d.in_stride = kBuf;
-        d.in_len = b.b.len;
-        d.out = b.b.out;
-        d.out_stride = kBuf;
-        d.out_cap = (uint64_t)k * kBuf;
-        d.out_len = b.b.olen;
-        if (hyobfs_salamander_deobfuscate_host(ctx, &d, 0) != HYOBFS_OK)
-            for (int i = 0; i < k; ++i) b.b.olen[i] = 0;   // nothing deobfuscated: every datagram dropped
-        received += (uint64_t)k;
-        ++rx_batches;
-        {
-            std::lock_guard<std::mutex> lk(rx_mu);
-            b.k = (uint32_t)k;
-            b.next = 0;
-            b.done.store(0, std::memory_order_relaxed);
-            ready.push_back(bi);
-        }
-        cv_ready.notify_all();
     }
+    // stopping: a kernel may still be writing the batch on the GPU, whose buffers
+    // are freed after this thread is joined
+    if (prev >= 0 && rx[prev].gpu_ok && zerocopy_on()) (void)gpu_queue_wait(gq_rx, prev);
 }
 
 Coalescer* coalescer_new(int fd, hyobfs_salamander* ctx, uint32_t max_batch, uint32_t max_wait_us,
@@ -352,13 +444,20 @@ Coalescer* coalescer_new(int fd, hyobfs_salamander* ctx, uint32_t max_batch, uin
     bool ok = true;
     for (auto& b : q->tx) ok = ok && b.alloc(max_batch);
     for (auto& b : q->rx) ok = ok && b.alloc(max_batch);
+    if (ok && zerocopy_on()) {
+        q->gq_tx = gpu_queue_new(ctx);
+        q->gq_rx = gpu_queue_new(ctx);
+        ok = q->gq_tx && q->gq_rx;
+    }
     if (!ok) {
+        gpu_queue_free(q->gq_tx);
+        gpu_queue_free(q->gq_rx);
         for (auto& b : q->tx) b.b.release();
         for (auto& b : q->rx) b.b.release();
         delete q;
         return nullptr;
     }
-    for (int i = 0; i < 3; ++i) q->freelist.push_back(i);
+    for (int i = 0; i < Coalescer::kRx; ++i) q->freelist.push_back(i);
     q->flusher = std::thread([q] { q->flush_loop(); });
     q->reader = std::thread([q] { q->read_loop(); });
     return q;
@@ -390,6 +489,8 @@ void coalescer_free(Coalescer* q) {
         q->cv_ready.notify_all();
         std::this_thread::yield();
     }
+    gpu_queue_free(q->gq_tx);   // (waits for its stream: nothing is left on it)
+    gpu_queue_free(q->gq_rx);
     for (auto& b : q->tx) b.b.release();
     for (auto& b : q->rx) b.b.release();
     delete q;

@@ -26,6 +26,20 @@ int64_t realtime_ns();
 void ctx_retain(hyobfs_salamander* ctx);
 void ctx_release(hyobfs_salamander* ctx);
 
+// Asynchronous batches for the coalescer (hyobfs_api.cpp): a stream and an event on
+// the context's device.  The coalescer's staging is mapped pinned host memory
+// (hyobfs_host_alloc), which the kernels read and write in place, so a batch is one
+// kernel launch on the coalescer's stream (hyobfs_salamander_*_batch) and a later
+// wait on the event recorded behind it: the host works on the previous batch (its
+// sendmmsg, or handing it to readers) while the GPU runs this one.
+struct GpuQueue;
+GpuQueue* gpu_queue_new(hyobfs_salamander* ctx);
+void gpu_queue_free(GpuQueue* g);
+// Launches the batch on the queue's stream and records event `slot` (0..3) behind it.
+int gpu_queue_submit(GpuQueue* g, const hyobfs_batch* b, bool obfuscate, int slot);
+// Waits for event `slot`: the batch submitted with it is done (and its output visible).
+int gpu_queue_wait(GpuQueue* g, int slot);
+
 // Starts the flusher and reader threads on fd.  nullptr on allocation failure.
 Coalescer* coalescer_new(int fd, hyobfs_salamander* ctx, uint32_t max_batch, uint32_t max_wait_us,
                          const Deadlines* dl);

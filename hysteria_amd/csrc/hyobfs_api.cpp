@@ -528,6 +528,49 @@ void ctx_release(hyobfs_salamander* c) {
     }
     delete c;
 }
+// ---- the coalescer's asynchronous batches (conn_coalesce.h)
+struct GpuQueue {
+    hyobfs_salamander* ctx = nullptr;
+    hipStream_t s = nullptr;
+    hipEvent_t ev[4] = {};
+};
+
+GpuQueue* gpu_queue_new(hyobfs_salamander* c) {
+    DeviceGuard g(c->device);
+    if (!g.ok) return nullptr;
+    auto* q = new (std::nothrow) GpuQueue();
+    if (!q) return nullptr;
+    q->ctx = c;
+    bool ok = hipStreamCreateWithFlags(&q->s, hipStreamNonBlocking) == hipSuccess;
+    for (auto& e : q->ev) ok = ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
+    if (!ok) {
+        gpu_queue_free(q);
+        return nullptr;
+    }
+    return q;
+}
+
+void gpu_queue_free(GpuQueue* q) {
+    if (!q) return;
+    DeviceGuard g(q->ctx->device);
+    if (q->s) (void)hipStreamSynchronize(q->s);
+    for (auto& e : q->ev)
+        if (e) (void)hipEventDestroy(e);
+    if (q->s) (void)hipStreamDestroy(q->s);
+    delete q;
+}
+
+int gpu_queue_submit(GpuQueue* q, const hyobfs_batch* b, bool obf, int slot) {
+    const int rc = run_batch(q->ctx, b, q->s, obf);
+    if (rc != HYOBFS_OK) return rc;
+    DeviceGuard g(q->ctx->device);
+    return hipEventRecord(q->ev[slot & 3], q->s) == hipSuccess ? HYOBFS_OK : HYOBFS_ERR_HIP;
+}
+
+int gpu_queue_wait(GpuQueue* q, int slot) {
+    return hipEventSynchronize(q->ev[slot & 3]) == hipSuccess ? HYOBFS_OK : HYOBFS_ERR_HIP;
+}
+
 }  // namespace hyobfs
 
 extern "C" {
@@ -539,7 +582,7 @@ void hyobfs_salamander_free(hyobfs_salamander* c) { hyobfs::ctx_release(c); }
 int hyobfs_salamander_device(const hyobfs_salamander* c) { return c ? c->device : -1; }
 
 int hyobfs_salamander_set_kernel(hyobfs_salamander* c, int kernel) {
-    if (!c || kernel < HYOBFS_KERNEL_AUTO || kernel > HYOBFS_KERNEL_TILE) return HYOBFS_ERR_INVALID;
+    if (!c || kernel < HYOBFS_KERNEL_AUTO || kernel > HYOBFS_KERNEL_FLAT) return HYOBFS_ERR_INVALID;
     c->kernel.store(kernel, std::memory_order_relaxed);
     return HYOBFS_OK;
 }
@@ -629,7 +672,7 @@ uint64_t hyobfs_batch_workspace_bytes(const hyobfs_batch* b) {
     bp.out_stride = b->out_stride;
     // the largest need over the kernel choices: independent of the context's
     uint64_t m = 0;
-    for (int k : {hyobfs::kKernelAuto, hyobfs::kKernelWave}) {
+    for (int k : {hyobfs::kKernelAuto, hyobfs::kKernelWave, hyobfs::kKernelFlat}) {
         bp.kernel = k;
         const uint64_t v = hyobfs::batch_workspace_bytes(true, bp);
         m = v > m ? v : m;

@@ -416,9 +416,10 @@ __global__ __launch_bounds__(256, HY_TILE_MIN_WAVES) void salamander_tile_kernel
 }
 
 // The tile kernel applies to slotted batches where every datagram has one
-// length, the slot, the input stride and the input base are multiples of 8, the
-// payload is at least 16 bytes, nothing is dropped, and no 16-byte chunk holds
-// payload bytes of two datagrams (deobfuscate into dense slots of 8 mod 16).
+// length, the slot, the input stride and the input base are multiples of 8
+// (every 8-byte half of an output chunk then belongs to one region: tile_half),
+// the input base is 16-aligned and a tile's input fits 64 KiB of LDS, the payload
+// is at least 16 bytes and nothing is dropped.
 template <bool OBF>
 inline bool tile_params(const BatchParams& b, TileParams& T) {
     if (b.out_stride == 0 || b.in_len || b.in_off || b.n == 0) return false;

@@ -16,6 +16,10 @@
 #   host            host-to-host rates (scripts/host_bench.py)
 #   pmc:LIB:WL:CTR  one rocprofv3 --pmc pass (counter CTR) of scripts/prof_one.py WL with the
 #                   library main or build_variants/libhyobfs_LIB.so
+#   clk:WL:K:PT     per-dispatch GPU clock: rocprofv3 --pmc GRBM_COUNT GRBM_GUI_ACTIVE --kernel-trace
+#                   of scripts/prof_one.py WL K (PT=1: output buffers pre-touched); scripts/clock_trace.py
+#   kt:WL:K         rocprofv3 --kernel-trace --stats of scripts/prof_one.py WL K (per-kernel times)
+#   udp:M:P:T:W     tools/udp_bench M P 4 1200 1024 T W (loopback PacketConn rate; M = batch|raw|coalesce|single)
 #   ab              in-process A/B of library builds (scripts/ab_variants.py; AB_* env vars)
 #   abg             the same for Gecko builds (scripts/ab_gecko_variants.py)
 set -u
@@ -57,6 +61,15 @@ for s in "$@"; do
             (cd /tmp && export TMPDIR=/tmp && export HYOBFS_LIB=$LIBP && step "pmc $LIBN $WL $CTR" 240 rocprofv3 \
               --pmc $CTR --kernel-trace --output-format csv -d "$O/pmc_${LIBN}_${WL}_$CTR" -o run -- \
               python3 "$R/scripts/prof_one.py" "$WL" 5 > "$O/pmc_${LIBN}_${WL}_$CTR.log" 2>&1) || exit 1 ;;
+    clk:*) IFS=: read -r _ WL K PT <<< "$s"
+            (cd /tmp && export TMPDIR=/tmp && export PROF_PRETOUCH=$PT && step "clk $WL $K $PT" 240 rocprofv3 \
+              --pmc GRBM_COUNT GRBM_GUI_ACTIVE --kernel-trace --output-format csv -d "$O/clk_${WL}_${K}_$PT" -o run -- \
+              python3 "$R/scripts/prof_one.py" "$WL" "$K" > "$O/clk_${WL}_${K}_$PT.log" 2>&1) || exit 1 ;;
+    kt:*) IFS=: read -r _ WL K <<< "$s"
+            (cd /tmp && export TMPDIR=/tmp && step "kt $WL $K" 240 rocprofv3 --kernel-trace --stats --output-format csv \
+              -d "$O/kt_${WL}_$K" -o run -- python3 "$R/scripts/prof_one.py" "$WL" "$K" > "$O/kt_${WL}_$K.log" 2>&1) || exit 1 ;;
+    udp:*) IFS=: read -r _ M P T W <<< "$s"
+            step "udp $M $P $T $W" 120 tools/udp_bench "$M" "$P" 4 1200 1024 "$T" "$W" > "$O/udp_${M}_${P}x${T}_w$W.json" ;;
     ab) step ab 600 python -u scripts/ab_variants.py ${AB_ARGS:-} > "$O/ab_${AB_NAME:-run}.txt" 2>&1 ;;
     abg) step abg 600 python -u scripts/ab_gecko_variants.py ${AB_ARGS:-} > "$O/abg_${AB_NAME:-run}.txt" 2>&1 ;;
     *) echo "unknown step $s"; exit 2 ;;

@@ -3,7 +3,8 @@ of the uniform 1M x 1200 B batch (BASELINE configs[1]), or of the 4M bimodal
 batch (configs[2], packed output) with 'bimodal' (contiguous input, as bench.py) or
 'bimodal_off' (explicit offsets); 'bimodal_alt': 20 warm-up obfuscate launches, then
 K of each layout alternating (obfuscate only).  Optional 3rd argument: the context's
-kernel (auto|wave|tile|stream)."""
+kernel (auto|wave|tile).  PROF_PRETOUCH=1 writes zeros over every output buffer (and
+the workspace) before the first launch (the first-touch study)."""
 import os, sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch, hysteria_amd
@@ -42,6 +43,10 @@ else:
               o.workspace_bytes(inp=inp, n=P, in_len=lens, out=wire, out_cap=cap),   # bimodal_alt: both layouts
               o.workspace_bytes(inp=wire, n=P, in_off=None if in_off is None else out_off, in_len=out_len, out=back, out_cap=total_in))
     ws = torch.empty(max(nws, 16), dtype=torch.uint8, device=dev)
+    if os.environ.get("PROF_PRETOUCH") == "1":
+        for t in (wire, out_off, out_len, back, ws):
+            t.zero_()
+        torch.cuda.synchronize()
     if wl == "bimodal_alt":   # 20 warm-up launches, then contiguous and explicit offsets alternating
         for i in range(20 + 2 * K):
             o.obfuscate_batch(inp, P, in_off=in_off if i % 2 else None, in_len=lens, salts=salts, out=wire,

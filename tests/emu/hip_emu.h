@@ -193,6 +193,12 @@ inline int hipMemcpyAsync(void* d, const void* s, size_t n, int, hipStream_t) { 
 inline unsigned long long atomicAdd(unsigned long long* p, unsigned long long v) {
     return __atomic_fetch_add(p, v, __ATOMIC_RELAXED);
 }
+inline unsigned long long atomicMax(unsigned long long* p, unsigned long long v) {
+    unsigned long long cur = __atomic_load_n(p, __ATOMIC_RELAXED);
+    while (cur < v && !__atomic_compare_exchange_n(p, &cur, v, false, __ATOMIC_RELAXED, __ATOMIC_RELAXED)) {
+    }
+    return cur;
+}
 
 #define hipLaunchKernelGGL(kernel, grid, block, shmem, stream, ...) \
     hyemu::launch(dim3(grid), dim3(block), (size_t)(shmem), [&] { kernel(__VA_ARGS__); })
@@ -228,6 +234,7 @@ inline hipError_t hipEventDestroy(hipEvent_t) { return hipSuccess; }
 inline hipError_t hipEventRecord(hipEvent_t, hipStream_t) { return hipSuccess; }   // launches run synchronously
 inline hipError_t hipStreamWaitEvent(hipStream_t, hipEvent_t, unsigned) { return hipSuccess; }
 inline hipError_t hipStreamSynchronize(hipStream_t) { return hipSuccess; }
+inline hipError_t hipEventSynchronize(hipEvent_t) { return hipSuccess; }
 inline hipError_t hipDeviceSynchronize() { return hipSuccess; }
 inline hipError_t hipMalloc(void** p, size_t n) {
     *p = std::malloc(n ? n : 1);

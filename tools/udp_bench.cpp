@@ -14,6 +14,8 @@
 // writer and `threads` reader threads per pair) on coalescing connections
 // (hyobfs_conn_set_coalescing: GPU batches of up to `batch` behind the calls).
 // Prints one JSON line.
+//   g++ -O2 -std=c++17 tools/udp_bench.cpp -Iinclude -Lhysteria_amd -lhyobfs \
+//       -Wl,-rpath,'$ORIGIN/../hysteria_amd' -lpthread -o tools/udp_bench
 #include <arpa/inet.h>
 #include <netinet/in.h>
 #include <string.h>
@@ -239,10 +241,10 @@ int main(int argc, char** argv) {
     auto pct = [&](double q) { return lat.empty() ? 0.0 : lat[(size_t)(q * (lat.size() - 1))] / 1e3; };
     for (auto& p : P) {
         bad += p.bad, calls += p.calls, sent += p.sent, recvd += p.recvd;
-        if (p.sc) hyobfs_conn_free(p.sc);
+        if (p.sc) hyobfs_conn_free(p.sc);   // a connection owns its fd: free closes it
         if (p.rc) hyobfs_conn_free(p.rc);
-        close(p.sfd);
-        close(p.rfd);
+        if (!p.sc) close(p.sfd);
+        if (!p.rc) close(p.rfd);
         hyobfs_salamander_free(p.sctx);
         hyobfs_salamander_free(p.rctx);
     }
