@@ -198,14 +198,6 @@ __device__ __forceinline__ uint64_t wave_sum(uint64_t x) {
     for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d, 64);
     return x;
 }
-__device__ __forceinline__ uint64_t wave_max_u64(uint64_t x) {
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) {
-        const uint64_t y = __shfl_xor(x, d, 64);
-        x = x > y ? x : y;
-    }
-    return x;
-}
 __device__ __forceinline__ uint32_t wave_max(uint32_t x) {
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) x = max(x, (uint32_t)__shfl_xor(x, d, 64));

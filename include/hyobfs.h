@@ -57,9 +57,8 @@ extern "C" {
 #endif
 
 /* ABI version.  3 (this header) against 2:
- *   - HYOBFS_KERNEL_STREAM is gone (the stream kernel lost to the wave-group
- *     kernel on every measured layout); 3 is now HYOBFS_KERNEL_FLAT, the kernel
- *     AUTO runs for contiguous input with packed output;
+ *   - HYOBFS_KERNEL_STREAM (3) is gone (the stream kernel lost to the wave-group
+ *     kernel on every measured layout); hyobfs_salamander_set_kernel rejects 3;
  *   - hyobfs_gecko_workspace_bytes is gone, and hyobfs_gecko_batch's workspace,
  *     workspace_bytes and out_cap are ignored (the Gecko wire-tile kernel is gone);
  *   - contiguous input with slotted output needs 2 x hyobfs_batch_workspace_size(n)
@@ -127,20 +126,18 @@ int hyobfs_salamander_device(const hyobfs_salamander* ctx);
    HYOBFS_KERNEL_AUTO runs the tile kernel on slotted batches whose region edges
    are all multiples of 8 (one length, slot and input stride multiples of 8,
    payloads of 16 bytes or more, nothing dropped) -- the uniform 1200-byte batch
-   of the benchmark --, the flat kernel on CONTIGUOUS input with packed output and
-   a 16-byte aligned `in` (the benchmark's bimodal batch), and the wave-group
-   kernel on every other batch (packed output with explicit offsets, ragged
-   lengths, any alignment).  HYOBFS_KERNEL_WAVE forces the wave-group kernel;
-   HYOBFS_KERNEL_TILE and HYOBFS_KERNEL_FLAT are AUTO.  The HYOBFS_KERNEL
-   environment variable (wave|tile|flat) overrides AUTO.  Returns
-   HYOBFS_ERR_INVALID for an unknown value.  May be called while other threads
-   run batches on the context (an atomic setting; a batch uses the value it read
-   when it started).  Outputs are identical. */
+   of the benchmark -- and the wave-group kernel on every other batch (packed
+   output, ragged lengths, any alignment; contiguous input scans its lengths
+   alongside the widths).  HYOBFS_KERNEL_WAVE forces the wave-group kernel;
+   HYOBFS_KERNEL_TILE is AUTO.  The HYOBFS_KERNEL environment variable
+   (wave|tile) overrides AUTO.  Returns HYOBFS_ERR_INVALID for an unknown value.
+   May be called while other threads run batches on the context (an atomic
+   setting; a batch uses the value it read when it started).  Outputs are
+   identical. */
 enum {
     HYOBFS_KERNEL_AUTO = 0,
     HYOBFS_KERNEL_WAVE = 1,
-    HYOBFS_KERNEL_TILE = 2,
-    HYOBFS_KERNEL_FLAT = 3
+    HYOBFS_KERNEL_TILE = 2
 };
 int hyobfs_salamander_set_kernel(hyobfs_salamander* ctx, int kernel);
 
@@ -229,13 +226,12 @@ typedef struct hyobfs_batch {
 uint64_t hyobfs_batch_workspace_size(uint64_t n);
 /* Scratch any batch needs, whatever the kernel choice: the above for packed
    batches with explicit offsets; for contiguous input twice that (width and
-   length sums), plus, with packed output, 16 + 24 x (ceil(out_cap / 8192) + 1)
-   bytes (the flat kernel's tile descriptors), or with slotted output (or
-   HYOBFS_PACKED_RUN_LOG2 shortening the wave kernel's packed runs) 8 B per
-   datagram (the input offsets a prepass writes); 0 for other slotted batches. */
+   length sums), plus 8 B per datagram (the input offsets a prepass writes) when
+   the output is slotted or HYOBFS_PACKED_RUN_LOG2 shortens the packed runs; 0 for
+   other slotted batches. */
 uint64_t hyobfs_batch_workspace_bytes(const hyobfs_batch* b);
 /* Which batch kernel a call with this batch would run under the context's
-   setting (HYOBFS_KERNEL_TILE, _FLAT or _WAVE; HYOBFS_KERNEL_AUTO for an
+   setting (HYOBFS_KERNEL_TILE or _WAVE; HYOBFS_KERNEL_AUTO for an
    empty batch), or a negative status for an invalid batch.  No device work:
    tests use it to prove which kernel their case exercised. */
 int hyobfs_salamander_batch_kernel(hyobfs_salamander* ctx, const hyobfs_batch* b, int obfuscate);

@@ -4,7 +4,7 @@ Every build runs in the same process on the same buffers, interleaved rounds,
 medians reported (placement moves a streaming kernel by +-5 %
 between processes).
 
-  AB_LIBS="main=hysteria_amd/libhyobfs.so,wave=build_variants/libhyobfs_gkwave.so,nopad!=..." \
+  AB_LIBS="main=hysteria_amd/libhyobfs.so,wave=ab_builds/libhyobfs_gkwave.so,nopad!=..." \
       python scripts/ab_gecko_variants.py
 
 A name ending in "!" is an ablation build (wrong output): its wire is not checked

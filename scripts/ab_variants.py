@@ -3,7 +3,7 @@ one workload: every variant runs in the same process on the same buffers, in
 interleaved rounds, medians reported -- buffer placement, which moves a
 streaming kernel by up to +-5 % between processes, is shared.
 
-  AB_LIBS="main=hysteria_amd/libhyobfs.so,align!=build_variants/libhyobfs_align.so" \
+  AB_LIBS="main=hysteria_amd/libhyobfs.so,align!=ab_builds/libhyobfs_align.so" \
       python scripts/ab_variants.py [kernels=tile] [L=1200] [P=1048576]
 
 A name ending in "!" is an ablation build (wrong output): its wire is not checked.

@@ -2,7 +2,9 @@
 
 GRBM_GUI_ACTIVE counts the GPU's busy cycles during a dispatch, GRBM_COUNT all of
 its cycles; divided by the dispatch's duration (Start/End_Timestamp, ns) they give
-the shader clock the dispatch ran at.  If a run of slow dispatches ran at the same
+the shader clock the dispatch ran at.  rocprofv3 sums the counter over the 8 XCDs
+(each has its own GRBM): the per-XCD clock is the sum / 8 (2.0-2.3 GHz measured,
+against the 2.4 GHz peak engine clock).  If a run of slow dispatches ran at the same
 clock as the fast ones, the slowdown is on the memory side, not the clock.
 
   python scripts/clock_trace.py gpurun_out/TAG/clk_bimodal_40_0 [kernel-substring]
@@ -31,7 +33,7 @@ def rows(d: str, match: str):
 def main():
     d = sys.argv[1]
     match = sys.argv[2] if len(sys.argv) > 2 else "salamander"
-    print("kind,index,duration_us,gui_active_MHz,grbm_count_MHz")
+    print("kind,index,duration_us,gui_active_MHz_sum8,grbm_count_MHz_sum8,clock_MHz_per_xcd")
     idx = {}
     for e in rows(d, match):
         kind = "obfuscate" if "<true" in e["name"] else "deobfuscate"
@@ -40,7 +42,7 @@ def main():
         us = (e["t1"] - e["t0"]) / 1e3
         ga = e.get("GRBM_GUI_ACTIVE", 0.0) / us
         gc = e.get("GRBM_COUNT", 0.0) / us
-        print(f"{kind},{i},{us:.1f},{ga:.0f},{gc:.0f}")
+        print(f"{kind},{i},{us:.1f},{ga:.0f},{gc:.0f},{gc / 8:.0f}")
 
 
 if __name__ == "__main__":

@@ -15,7 +15,7 @@
 #   auxpmc          VALU counters of the (f)-row kernels
 #   host            host-to-host rates (scripts/host_bench.py)
 #   pmc:LIB:WL:CTR  one rocprofv3 --pmc pass (counter CTR) of scripts/prof_one.py WL with the
-#                   library main or build_variants/libhyobfs_LIB.so
+#                   library main or ab_builds/libhyobfs_LIB.so
 #   clk:WL:K:PT     per-dispatch GPU clock: rocprofv3 --pmc GRBM_COUNT GRBM_GUI_ACTIVE --kernel-trace
 #                   of scripts/prof_one.py WL K (PT=1: output buffers pre-touched); scripts/clock_trace.py
 #   kt:WL:K         rocprofv3 --kernel-trace --stats of scripts/prof_one.py WL K (per-kernel times)
@@ -57,7 +57,7 @@ for s in "$@"; do
     host) step host 600 python -u scripts/host_bench.py > "$O/host_bench.json" 2> "$O/host_bench.err" ;;
     pmc:*) IFS=: read -r _ LIBN WL CTR <<< "$s"
             LIBP=$R/hysteria_amd/libhyobfs.so
-            [ "$LIBN" = main ] || LIBP=$R/build_variants/libhyobfs_$LIBN.so
+            [ "$LIBN" = main ] || LIBP=$R/ab_builds/libhyobfs_$LIBN.so
             (cd /tmp && export TMPDIR=/tmp && export HYOBFS_LIB=$LIBP && step "pmc $LIBN $WL $CTR" 240 rocprofv3 \
               --pmc $CTR --kernel-trace --output-format csv -d "$O/pmc_${LIBN}_${WL}_$CTR" -o run -- \
               python3 "$R/scripts/prof_one.py" "$WL" 5 > "$O/pmc_${LIBN}_${WL}_$CTR.log" 2>&1) || exit 1 ;;

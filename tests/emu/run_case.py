@@ -140,16 +140,10 @@ def case_contig(seed, n, dist, obf, cap_pct, psk_len, pkt_cap=0, misalign=0, out
         assert np.array_equal(woff[1:], np.cumsum(wlen[:-1], dtype=np.uint64))
         inp, in_off, lens, total = winp, woff, np.ascontiguousarray(wlen, np.uint32), wl
     full = n * out_stride if out_stride else total + (8 * n if obf else 0)
-    cap = max(16, full * cap_pct // 100)
     tsums = ((n + 255) // 256 + 1) * 8
-    flat = not out_stride and not misalign and os.environ.get("HYOBFS_KERNEL") != "wave"
     prepass = out_stride or os.environ.get("HYOBFS_PACKED_RUN_LOG2", "6") != "6"
-    # hyobfs_batch_workspace_bytes: the largest need over the kernel choices
-    ws = 2 * tsums + (8 * n if prepass else 0)   # the wave kernel's
-    if not out_stride and not misalign:           # the flat kernel's tile descriptors
-        ws = max(ws, 2 * tsums + 16 + 24 * ((cap + 8191) // 8192 + 1))
-    run(obf, psk, lens, in_off, inp, salts, cap, pkt_cap=pkt_cap, contiguous=True,
-        out_stride=out_stride, expect_kernel="flat" if flat else "wave", expect_ws=ws)
+    run(obf, psk, lens, in_off, inp, salts, max(16, full * cap_pct // 100), pkt_cap=pkt_cap, contiguous=True,
+        out_stride=out_stride, expect_kernel="wave", expect_ws=2 * tsums + (8 * n if prepass else 0))
 
 
 def case_bimodal(n, obf):

@@ -150,18 +150,16 @@ PACKED_CASES = [
 
 # Contiguous input (in_off NULL, in_stride 0; tests/emu/run_case.py case_contig:
 # seed n dist obf cap% psk_len [pkt_cap misalign out_stride]).  Packed output under
-# AUTO: the flat kernel (salamander_flat.h; the misaligned cases: the wave kernel
-# taking its input offsets from the scan of the lengths); packed runs of 8 or slotted
-# output: the prepass's input offsets (in_offsets_kernel), then the wave kernel.
-# Sizes are small (each emulated flat workgroup is 256 host threads); dist 2 (0..40 B)
-# still gives tiles of several passes, the GPU tier runs the grid at 8-20k datagrams.  Bimodal, 0..2100 B, tiny (several datagrams per chunk), 1-5 KB,
+# AUTO: the wave kernel taking its input offsets from the scan of the lengths; packed
+# runs of 8 or slotted output: the prepass's input offsets (in_offsets_kernel), then
+# the wave kernel.  Bimodal, 0..2100 B, tiny (several datagrams per chunk), 1-5 KB,
 # zero-length datagrams; out_cap cuts, pkt_cap drops, real wire with 8-byte
 # datagrams, PSKs across salt words and the two-block case, a misaligned input.
 CONTIG_CASES = [
-    "1 1000 0 1 100 16", "2 1000 0 0 100 16", "3 700 1 1 100 16", "4 700 1 0 100 33", "5 1000 2 1 100 16",
-    "6 1000 2 0 100 121", "7 300 3 1 100 16", "8 300 3 0 100 4", "9 1000 4 1 100 16", "10 1000 4 0 100 16",
-    "11 700 1 1 60 16", "12 700 1 0 70 127", "13 700 1 1 100 16 1000", "14 700 1 0 100 16 900",
-    "15 1000 0 1 100 16 0 1", "16 1000 0 0 100 16 0 1", "17 1000 2 1 50 16",
+    "1 3000 0 1 100 16", "2 3000 0 0 100 16", "3 2000 1 1 100 16", "4 2000 1 0 100 33", "5 3000 2 1 100 16",
+    "6 3000 2 0 100 121", "7 300 3 1 100 16", "8 300 3 0 100 4", "9 3000 4 1 100 16", "10 3000 4 0 100 16",
+    "11 2000 1 1 60 16", "12 2000 1 0 70 127", "13 2000 1 1 100 16 1000", "14 2000 1 0 100 16 900",
+    "15 3000 0 1 100 16 0 1", "16 3000 0 0 100 16 0 1", "17 3000 2 1 50 16",
 ]
 
 
