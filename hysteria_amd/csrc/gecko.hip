@@ -44,6 +44,9 @@ __device__ __forceinline__ gk_u128 gk_mask(uint32_t lo, uint32_t hi) {   // byte
 #ifndef HY_GK_U
 #define HY_GK_U 4
 #endif
+#ifndef HY_GK_EDGE_KS
+#define HY_GK_EDGE_KS 1   // edge chunks' padding keystream computed by lane quads up front (not one lane per block)
+#endif
 constexpr int kGkU = HY_GK_U;   // windows per lane in flight
 
 struct GeckoGroup {             // one wave's 64 frames, in LDS
@@ -55,6 +58,10 @@ struct GeckoGroup {             // one wave's 64 frames, in LDS
     uint32_t rs[65];            // aligned path: wire start relative to the group base, [64] = end of all
     uint64_t salt[64];          // aligned path: the salts (merged into the edge chunks)
     gk_u128 key[128];           // the frame's key, two halves (aligned path: rotated to the wire phase)
+#if HY_GK_EDGE_KS
+    gk_u128 eks[128];           // aligned path: keystream of frame k's edge chunks holding padding
+                                // ([2k] the pad's first chunk, [2k + 1] its last), four lanes per block
+#endif
 };
 
 // ---- padding keystream (include/hyobfs_gecko.h): ChaCha, 8 rounds, RFC 8439 block
@@ -173,9 +180,16 @@ __device__ __forceinline__ void gk_contrib(const hyobfs_gecko_batch& B, const Gk
             X |= (p0 <= 0 ? H << (8 * -p0) : H >> (8 * p0)) & gk_mask(xlo - p0, hhi - p0);
         }
         const int32_t plo = max(p0, (int32_t)HYOBFS_GECKO_HEADER_LEN), phi = min(p0 + 16, hp);
-        if (plo < phi)   // the 16-aligned wire chunk at base + a is one keystream column
+        if (plo < phi) {   // the 16-aligned wire chunk at base + a is one keystream column
+#if HY_GK_EDGE_KS
+            // an edge chunk holding padding is the pad's first or last chunk (precomputed)
+            const uint32_t c0 = (rs + HYOBFS_SALT_LEN + HYOBFS_GECKO_HEADER_LEN) >> 4;
+            X |= G.eks[2 * k + ((a >> 4) == c0 ? 0u : 1u)] & gk_mask(plo - p0, phi - p0);
+#else
             X |= gk_ks_single(P, (base + a) >> 6, (uint32_t)((base + a) >> 4) & 3u) &
                  gk_mask(plo - p0, phi - p0);
+#endif
+        }
         const int32_t clo = max(p0, hp);
         if (clo < xhi) {   // chunk bytes
             const uint8_t* __restrict__ ch = B.msg + G.chunk_off[k];
@@ -224,6 +238,33 @@ __device__ __forceinline__ void gecko_encode_aligned(const KeyParams& K, const h
         G.key[2 * lane + 1] = (gk_u128)kr[3] << 64 | kr[2];
         G.salt[lane] = salt;
     }
+#if HY_GK_EDGE_KS
+    // ---- the keystream columns of the edge chunks that hold padding: frame l's pad
+    // runs over wire [rs + 13, rs + 8 + hp); its first and last chunk are edges unless
+    // wholly padding (then the sweep covers them).  Sixteen such columns per pass, one
+    // lane quad per 64-byte block (gk_ks_quad); single-lane blocks cost 4x the VALU.
+    {
+        uint32_t need0 = ~0u, need1 = ~0u;   // group-relative chunk indices
+        if (valid) {
+            const uint32_t hp = G.hp_plain[lane] & 0xffff;
+            const uint32_t ps = rs + HYOBFS_SALT_LEN + HYOBFS_GECKO_HEADER_LEN, pe = rs + HYOBFS_SALT_LEN + hp;
+            if (pe > ps) {
+                const uint32_t c0 = ps >> 4, c1 = (pe - 1) >> 4;
+                if ((ps & 15u) || 16u * c0 + 16u > pe) need0 = c0;
+                if (c1 != c0 && (pe & 15u)) need1 = c1;
+            }
+        }
+        const unsigned long long any = __ballot(need0 != ~0u || need1 != ~0u);
+        const uint32_t last = any ? 63u - (uint32_t)__builtin_clzll(any) : 0u;   // last frame with a need
+        for (uint32_t j = 0; any && j * 8u <= last; ++j) {   // pass j: needs 16 j .. 16 j + 15 (frames 8 j ..)
+            const uint32_t n = j * 16u + (lane >> 2), fr = n >> 1;
+            const uint32_t n0 = __shfl(need0, (int)fr, 64), n1 = __shfl(need1, (int)fr, 64);
+            const uint32_t c = (n & 1u) ? n1 : n0;
+            const gk_u128 ks = gk_ks_quad(P, (base + 16ull * (c == ~0u ? 0u : c)) >> 6, lane & 3u);
+            if (c != ~0u && (lane & 3u) == (c & 3u)) G.eks[n] = ks;
+        }
+    }
+#endif
     hy_wave_sync();
     uint8_t* __restrict__ ob = B.out + base;
     const uint32_t tc = (rend + 15) >> 4;   // chunks of the group's wire range

@@ -8,8 +8,7 @@ between processes).
       python scripts/ab_gecko_variants.py
 
 A name ending in "!" is an ablation build (wrong output): its wire is not checked
-against the first build's.  AB_GK_MODES (default "tile,wave") runs each build through
-the wire-tile kernel (out_cap given) and the wave-group kernel (no out_cap)."""
+against the first build's."""
 import os
 import statistics
 import sys
