@@ -277,7 +277,12 @@ int hyobfs_shard_bounds(const uint32_t* in_len, uint64_t n, int nshards, uint64_
  * chunk k and the device-to-host copy of chunk k-1 overlap.  Synchronous:
  * returns when every output byte is in host memory.  Host buffers allocated
  * with hyobfs_host_alloc (pinned) copy at full PCIe rate; pageable memory
- * works but is staged by the runtime.
+ * works but is staged by the runtime.  The device-to-host copy moves whole
+ * output slots: bytes of a slot past out_len[i] are unspecified afterwards.
+ * When in, out, in_len, salts (obfuscate) and out_len are ALL device-mapped
+ * host memory (hyobfs_host_alloc), the batch instead runs as one batch call
+ * on the mapped pointers (zero-copy, `chunk` unused; HYOBFS_HOST_ZEROCOPY=0
+ * turns this off) and, like the device batches, writes only the regions.
  */
 int hyobfs_salamander_obfuscate_host(hyobfs_salamander* ctx, const hyobfs_batch* b,
                                      uint64_t chunk);

@@ -179,10 +179,10 @@ def test_emulated_contiguous_input_prepass_offsets(emu_lib, args):
 # into 1200-byte slots (the slot drops the long ones), out_cap cutting the slots,
 # pkt_cap drops, a misaligned input, a two-block PSK, tiny datagrams in 48-byte slots.
 CONTIG_SLOTTED = [
-    "21 3000 0 1 100 16 0 0 1358", "22 3000 0 0 100 16 0 0 1350", "23 2000 1 1 100 16 0 0 1200",
-    "24 2000 1 0 100 33 0 0 1200", "25 2000 1 1 60 16 0 0 2112", "26 2000 1 0 70 127 0 0 2104",
-    "27 2000 1 1 100 16 900 0 1208", "28 2000 1 0 100 16 700 1 2104", "29 3000 2 1 100 121 0 0 48",
-    "30 3000 4 0 100 16 0 0 1350",
+    "21 1000 0 1 100 16 0 0 1358", "22 1000 0 0 100 16 0 0 1350", "23 800 1 1 100 16 0 0 1200",
+    "24 800 1 0 100 33 0 0 1200", "25 800 1 1 60 16 0 0 2112", "26 800 1 0 70 127 0 0 2104",
+    "27 800 1 1 100 16 900 0 1208", "28 800 1 0 100 16 700 1 2104", "29 1000 2 1 100 121 0 0 48",
+    "30 1000 4 0 100 16 0 0 1350",
 ]
 
 

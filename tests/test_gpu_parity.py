@@ -749,11 +749,33 @@ def test_packed_offsets_past_one_scan_pass(obfs, gpu):
         assert got == ref.obfuscate(PSK, h_in[p * L:(p + 1) * L].tobytes(), int(h_salts[p]).to_bytes(8, "little")), p
 
 
+class _Mapped:
+    """numpy views of mapped pinned host buffers (hyobfs_host_alloc), freed on close."""
+
+    def __init__(self):
+        from hysteria_amd import _lib
+        self.lib, self.ptrs = _lib.load(), []
+
+    def array(self, n, dtype):
+        import ctypes
+        nb = n * np.dtype(dtype).itemsize
+        p = self.lib.hyobfs_host_alloc(nb)
+        assert p, "hyobfs_host_alloc"
+        self.ptrs.append(p)
+        return np.ctypeslib.as_array(ctypes.cast(p, ctypes.POINTER(ctypes.c_uint8)), (nb,)).view(dtype)
+
+    def close(self):
+        for p in self.ptrs:
+            self.lib.hyobfs_host_free(p)
+
+
 @pytest.mark.parametrize("obf", [True, False])
-@pytest.mark.parametrize("pinned", [True, False])
-def test_host_batch_pipeline_vs_oracle(obfs, gpu, obf, pinned):
-    """Host-resident slotted batch (recvmmsg/sendmmsg ring shape) through the
-    H2D / kernel / D2H pipeline, chunked so several chunks cycle the 3 slots."""
+@pytest.mark.parametrize("mem", ["pinned", "pageable", "mapped"])
+def test_host_batch_pipeline_vs_oracle(obfs, gpu, obf, mem):
+    """Host-resident slotted batch (recvmmsg/sendmmsg ring shape): pageable and torch-pinned
+    buffers (with pageable lengths / salts / out_len) through the H2D / kernel / D2H
+    pipeline, chunked so several chunks cycle the 3 slots; every array in mapped pinned
+    memory (hyobfs_host_alloc) through the zero-copy path: one batch call in place."""
     import torch
     n, L = 5000, 1350
     rng = np.random.default_rng(7 + obf)
@@ -763,25 +785,42 @@ def test_host_batch_pipeline_vs_oracle(obfs, gpu, obf, pinned):
     inp = rng.integers(0, 256, n * stride_in, dtype=np.uint8)
     salts = ref.splitmix64_array(2, 0, n)
     out_stride = 2048
-    if pinned:
-        t_in = torch.from_numpy(inp).pin_memory()
-        t_out = torch.full((n * out_stride,), 0xA5, dtype=torch.uint8).pin_memory()
-        in_buf, out_buf = t_in, t_out
-    else:
-        in_buf, out_buf = inp, np.full(n * out_stride, 0xA5, np.uint8)
     out_len = np.zeros(n, np.uint32)
-    kw = dict(in_stride=stride_in, in_len=lens, out=out_buf, out_stride=out_stride, out_len=out_len, chunk=777)
-    if obf:
-        obfs.obfuscate_host(in_buf, n, salts=salts, **kw)
-    else:
-        obfs.deobfuscate_host(in_buf, n, **kw)
-    got = out_buf.numpy() if pinned else out_buf
+    h_lens, h_salts = lens.copy(), salts.copy()   # the host copies the check reads
+    mapped = _Mapped()
+    try:
+        if mem == "pinned":
+            in_buf = torch.from_numpy(inp).pin_memory()
+            out_buf = torch.full((n * out_stride,), 0xA5, dtype=torch.uint8).pin_memory()
+        elif mem == "mapped":
+            in_buf, out_buf = mapped.array(n * stride_in, np.uint8), mapped.array(n * out_stride, np.uint8)
+            in_buf[:] = inp
+            out_buf[:] = 0xA5
+            lens, salts, out_len = mapped.array(n, np.uint32), mapped.array(n, np.uint64), mapped.array(n, np.uint32)
+            lens[:], salts[:], out_len[:] = h_lens, h_salts, 0
+        else:
+            in_buf, out_buf = inp, np.full(n * out_stride, 0xA5, np.uint8)
+        kw = dict(in_stride=stride_in, in_len=lens, out=out_buf, out_stride=out_stride, out_len=out_len, chunk=777)
+        if obf:
+            obfs.obfuscate_host(in_buf, n, salts=salts, **kw)
+        else:
+            obfs.deobfuscate_host(in_buf, n, **kw)
+        got = np.array(out_buf.numpy() if mem == "pinned" else out_buf)
+        olen = np.array(out_len)
+    finally:
+        mapped.close()
     for i in range(n):
-        src = inp[i * stride_in:i * stride_in + int(lens[i])].tobytes()
-        exp = ref.obfuscate(PSK, src, int(salts[i]).to_bytes(8, "little"), out_stride) if obf \
+        src = inp[i * stride_in:i * stride_in + int(h_lens[i])].tobytes()
+        exp = ref.obfuscate(PSK, src, int(h_salts[i]).to_bytes(8, "little"), out_stride) if obf \
             else ref.deobfuscate(PSK, src, out_stride)
-        assert int(out_len[i]) == len(exp), i
+        assert int(olen[i]) == len(exp), i
         assert got[i * out_stride:i * out_stride + len(exp)].tobytes() == exp, i
+    if mem != "mapped":
+        return   # the staged pipeline copies whole output slots back (include/hyobfs.h)
+    untouched = np.ones(n * out_stride, bool)   # zero-copy writes only the regions
+    for i in range(n):
+        untouched[i * out_stride:i * out_stride + int(olen[i])] = False
+    assert (got[untouched] == 0xA5).all()
 
 
 @pytest.mark.gpu
