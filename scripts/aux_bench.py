@@ -21,16 +21,22 @@ dev = torch.device("cuda:0")
 K = 20
 
 
-def timed(fn):
-    fn()
+def timed(fn, warmup=20, rounds=5):
+    """Steady state: `warmup` untimed calls first (the shader clock ramps up over the first
+    launches), then the median over `rounds` of K back-to-back calls."""
+    for _ in range(warmup):
+        fn()
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(K):
-        fn()
-    e1.record()
-    torch.cuda.synchronize()
-    return e0.elapsed_time(e1) / K
+    ts = []
+    for _ in range(rounds):
+        e0.record()
+        for _ in range(K):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        ts.append(e0.elapsed_time(e1) / K)
+    return sorted(ts)[len(ts) // 2]
 
 
 def d(a):

@@ -29,6 +29,9 @@ TAG=${1:?tag}
 shift
 O=$R/gpurun_out/$TAG
 mkdir -p "$O"
+# the shipped library must be built from these sources (its build id is the source hash)
+SHA=$(python3 scripts/src_sha.py)
+grep -q "$SHA" hysteria_amd/libhyobfs.so || { echo "libhyobfs.so is not built from these sources ($SHA): rebuild"; exit 3; }
 exec 3>&1   # step markers go to the session's stdout, not into a step's redirected output
 step() {
   local name=$1 lim=$2; shift 2
