@@ -18,6 +18,7 @@
 #                   library main or ab_builds/libhyobfs_LIB.so
 #   clk:WL:K:PT     per-dispatch GPU clock: rocprofv3 --pmc GRBM_COUNT GRBM_GUI_ACTIVE --kernel-trace
 #                   of scripts/prof_one.py WL K (PT=1: output buffers pre-touched); scripts/clock_trace.py
+#   clkbench:W      the same counters over the bench command (bench.py --steps 20 --warmup W)
 #   kt:WL:K         rocprofv3 --kernel-trace --stats of scripts/prof_one.py WL K (per-kernel times)
 #   udp:M:P:T:W     tools/udp_bench M P 4 1200 1024 T W (loopback PacketConn rate; M = batch|raw|coalesce|single)
 #   ab              in-process A/B of library builds (scripts/ab_variants.py; AB_* env vars)
@@ -68,6 +69,10 @@ for s in "$@"; do
             (cd /tmp && export TMPDIR=/tmp && export PROF_PRETOUCH=$PT && step "clk $WL $K $PT" 240 rocprofv3 \
               --pmc GRBM_COUNT GRBM_GUI_ACTIVE --kernel-trace --output-format csv -d "$O/clk_${WL}_${K}_$PT" -o run -- \
               python3 "$R/scripts/prof_one.py" "$WL" "$K" > "$O/clk_${WL}_${K}_$PT.log" 2>&1) || exit 1 ;;
+    clkbench:*) IFS=: read -r _ W <<< "$s"   # the bench command itself, W warmup steps
+            (cd /tmp && export TMPDIR=/tmp && step "clkbench $W" 240 rocprofv3 \
+              --pmc GRBM_COUNT GRBM_GUI_ACTIVE --kernel-trace --output-format csv -d "$O/clkbench_$W" -o run -- \
+              python3 "$R/bench.py" --steps 20 --warmup "$W" --no-cpu-baseline --no-parity > "$O/clkbench_$W.log" 2>&1) || exit 1 ;;
     kt:*) IFS=: read -r _ WL K <<< "$s"
             (cd /tmp && export TMPDIR=/tmp && step "kt $WL $K" 240 rocprofv3 --kernel-trace --stats --output-format csv \
               -d "$O/kt_${WL}_$K" -o run -- python3 "$R/scripts/prof_one.py" "$WL" "$K" > "$O/kt_${WL}_$K.log" 2>&1) || exit 1 ;;
