@@ -4,19 +4,31 @@ batch (configs[2], packed output) with 'bimodal' (contiguous input, as bench.py)
 'bimodal_off' (explicit offsets); 'bimodal_alt': 20 warm-up obfuscate launches, then
 K of each layout alternating (obfuscate only).  Optional 3rd argument: the context's
 kernel (auto|wave|tile).  PROF_PRETOUCH=1 writes zeros over every output buffer (and
-the workspace) before the first launch (the first-touch study)."""
+the workspace) before the first launch (the first-touch study).
+'uniform_rev': the uniform batch with the K deobfuscate launches first (a wire made by
+one obfuscate launch), then the K obfuscate launches."""
 import os, sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch, hysteria_amd
 wl = sys.argv[1] if len(sys.argv) > 1 else "uniform"
 K = int(sys.argv[2]) if len(sys.argv) > 2 else 5
 kern = sys.argv[3] if len(sys.argv) > 3 else "auto"
-if wl not in ("uniform", "bimodal", "bimodal_off", "bimodal_alt"):
-    sys.exit(f"unknown workload {wl!r}: uniform | bimodal | bimodal_off | bimodal_alt")
+if wl not in ("uniform", "uniform_rev", "bimodal", "bimodal_off", "bimodal_alt"):
+    sys.exit(f"unknown workload {wl!r}: uniform | uniform_rev | bimodal | bimodal_off | bimodal_alt")
 dev = torch.device("cuda:0")
 o = hysteria_amd.SalamanderObfuscator(b"average_password", 0)
 o.set_kernel(kern)
-if wl == "uniform":
+if wl == "uniform_rev":
+    P, L = 1 << 20, 1200
+    inp = torch.empty(P * L, dtype=torch.uint8, device=dev); hysteria_amd.synth_stream(inp, P * L, 1, 0)
+    salts = torch.empty(P, dtype=torch.int64, device=dev); hysteria_amd.synth_u64(salts, P, 2, 0)
+    wire = torch.empty(P * (L + 8), dtype=torch.uint8, device=dev); back = torch.empty(P * L, dtype=torch.uint8, device=dev)
+    o.obfuscate_batch(inp, P, in_stride=L, len_uniform=L, salts=salts, out=wire, out_stride=L + 8)
+    for _ in range(K):
+        o.deobfuscate_batch(wire, P, in_stride=L + 8, len_uniform=L + 8, out=back, out_stride=L)
+    for _ in range(K):
+        o.obfuscate_batch(inp, P, in_stride=L, len_uniform=L, salts=salts, out=wire, out_stride=L + 8)
+elif wl == "uniform":
     P, L = 1 << 20, 1200
     inp = torch.empty(P * L, dtype=torch.uint8, device=dev); hysteria_amd.synth_stream(inp, P * L, 1, 0)
     salts = torch.empty(P, dtype=torch.int64, device=dev); hysteria_amd.synth_u64(salts, P, 2, 0)
