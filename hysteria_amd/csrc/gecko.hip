@@ -42,7 +42,16 @@ __device__ __forceinline__ gk_u128 gk_mask(uint32_t lo, uint32_t hi) {   // byte
 #define HY_GK_PIPE 1   // software-pipelined aligned sweep (two iterations' loads in flight)
 #endif
 #ifndef HY_GK_U
-#define HY_GK_U 4
+#define HY_GK_U 3   // with HY_GK_REC, 4 spills at the 5-wave register cap
+#endif
+#ifndef HY_GK_REC
+#define HY_GK_REC 1   // aligned sweep: one 16-byte LDS record per frame (wire start, lengths, chunk offset)
+#endif
+#ifndef HY_GK_ABL
+#define HY_GK_ABL 0   // ablations (wrong output, timing only): 1 no key hash, 2 no edge chunks, 4 no edge keystream
+#endif
+#ifndef HY_GK_MERGE
+#define HY_GK_MERGE 1   // aligned sweep: padding and message chunks leave through one conditional store
 #endif
 #ifndef HY_GK_EDGE_KS
 #define HY_GK_EDGE_KS 1   // edge chunks' padding keystream computed by lane quads up front (not one lane per block)
@@ -50,10 +59,15 @@ __device__ __forceinline__ gk_u128 gk_mask(uint32_t lo, uint32_t hi) {   // byte
 constexpr int kGkU = HY_GK_U;   // windows per lane in flight
 
 struct GeckoGroup {             // one wave's 64 frames, in LDS
-    uint64_t out_off[64];       // wire datagram start
+    union {
+        struct {                // plaintext-window path
+            uint64_t out_off[64];   // wire datagram start
+            uint32_t wstart[65];    // first plaintext window of the frame (exclusive scan), [64] = total
+        };
+        uint4 rec[65];          // aligned path (HY_GK_REC): {rs, hp_plain, chunk_off lo, hi}, [64] = sentinel
+    };
     uint64_t chunk_off[64];
     uint64_t hdr[64];           // the 5 header bytes, little-endian in the low bytes
-    uint32_t wstart[65];        // first plaintext window of the frame (exclusive scan), [64] = total
     uint32_t hp_plain[64];      // chunk start (low 16 bits) | plaintext length (high 16 bits)
     uint32_t rs[65];            // aligned path: wire start relative to the group base, [64] = end of all
     uint64_t salt[64];          // aligned path: the salts (merged into the edge chunks)
@@ -230,6 +244,13 @@ __device__ __forceinline__ void gecko_encode_aligned(const KeyParams& K, const h
     G.rs[lane] = rs;
     if (lane == 0) G.rs[64] = rend;
     if (!valid) G.hp_plain[lane] = 0;
+#if HY_GK_REC
+    {   // (out_off, which this overlays, is not read on the aligned path)
+        const uint64_t co = valid ? G.chunk_off[lane] : 0ull;
+        G.rec[lane] = make_uint4(rs, valid ? G.hp_plain[lane] : 0u, (uint32_t)co, (uint32_t)(co >> 32));
+        if (lane == 0) G.rec[64] = make_uint4(0xFFFFFFFFu, 0u, 0u, 0u);   // stops every walk
+    }
+#endif
     if (valid) {   // the key rotated so that rel address (a + b) mod 32 indexes it
         const uint64_t kw[4] = {(uint64_t)k0, (uint64_t)(k0 >> 64), (uint64_t)k1, (uint64_t)(k1 >> 64)};
         uint64_t kr[4];
@@ -241,8 +262,9 @@ __device__ __forceinline__ void gecko_encode_aligned(const KeyParams& K, const h
 #if HY_GK_EDGE_KS
     // ---- the keystream columns of the edge chunks that hold padding: frame l's pad
     // runs over wire [rs + 13, rs + 8 + hp); its first and last chunk are edges unless
-    // wholly padding (then the sweep covers them).  Sixteen such columns per pass, one
-    // lane quad per 64-byte block (gk_ks_quad); single-lane blocks cost 4x the VALU.
+    // wholly padding (then the sweep covers them).  One column per lane, 64 per pass
+    // (gk_ks_single: a whole block, one column kept); lane quads that keep one column
+    // of four ran 2.3 % slower (profiles/r05_abg_gecko_sweep_records.txt).
     {
         uint32_t need0 = ~0u, need1 = ~0u;   // group-relative chunk indices
         if (valid) {
@@ -254,14 +276,13 @@ __device__ __forceinline__ void gecko_encode_aligned(const KeyParams& K, const h
                 if (c1 != c0 && (pe & 15u)) need1 = c1;
             }
         }
-        const unsigned long long any = __ballot(need0 != ~0u || need1 != ~0u);
+        const unsigned long long any = (HY_GK_ABL & 4) ? 0ull : __ballot(need0 != ~0u || need1 != ~0u);
         const uint32_t last = any ? 63u - (uint32_t)__builtin_clzll(any) : 0u;   // last frame with a need
-        for (uint32_t j = 0; any && j * 8u <= last; ++j) {   // pass j: needs 16 j .. 16 j + 15 (frames 8 j ..)
-            const uint32_t n = j * 16u + (lane >> 2), fr = n >> 1;
+        for (uint32_t j = 0; any && j * 32u <= last; ++j) {   // pass j: needs 64 j .. 64 j + 63 (frames 32 j ..)
+            const uint32_t n = j * 64u + lane, fr = n >> 1;
             const uint32_t n0 = __shfl(need0, (int)fr, 64), n1 = __shfl(need1, (int)fr, 64);
             const uint32_t c = (n & 1u) ? n1 : n0;
-            const gk_u128 ks = gk_ks_quad(P, (base + 16ull * (c == ~0u ? 0u : c)) >> 6, lane & 3u);
-            if (c != ~0u && (lane & 3u) == (c & 3u)) G.eks[n] = ks;
+            if (c != ~0u) G.eks[n] = gk_ks_single(P, (base + 16ull * c) >> 6, c & 3u);
         }
     }
 #endif
@@ -280,7 +301,7 @@ __device__ __forceinline__ void gecko_encode_aligned(const KeyParams& K, const h
     // still in the L2 when the sweep's streaming stores complete it): the first two (salt, header), the one holding
     // the padding/chunk seam, the last; a chunk an earlier frame reaches into is that
     // frame's, and its owner merges every frame that touches it
-    if (valid) {
+    if (valid && !(HY_GK_ABL & 2)) {
         const uint32_t hp = G.hp_plain[lane] & 0xffff;
         const uint32_t cs = rs >> 4, ce = (rs + HYOBFS_SALT_LEN + plain - 1) >> 4;
         const uint32_t seam = (rs + HYOBFS_SALT_LEN + hp - 1) >> 4;
@@ -320,6 +341,34 @@ __device__ __forceinline__ void gecko_encode_aligned(const KeyParams& K, const h
         uint8_t kind[kGkU];   // 0 nothing, 1 padding, 2 message bytes
     };
     uint32_t q = 0;
+#if HY_GK_REC
+    // the lane's frame record and the next one's stay in registers: a window moves
+    // forward by 64 chunks, so the walk reads one record per frame passed (the sentinel
+    // rec[64] stops it) and the classification needs no further LDS read
+    uint4 rq = G.rec[0];
+    uint32_t rnx = G.rec[1].x;   // the next frame's wire start
+    const uint8_t* const safe = hy_safe_line();
+    auto issue = [&](uint32_t T, Step& S) {
+#pragma unroll
+        for (int u = 0; u < kGkU; ++u) {
+            const uint32_t c = T + lane + 64 * u, a = 16 * c;
+            while (rnx <= a) {
+                ++q;
+                rq = G.rec[q];
+                rnx = G.rec[q + 1].x;
+            }
+            const int32_t hp = (int32_t)(rq.y & 0xffff), pl = (int32_t)(rq.y >> 16);
+            const int32_t p = (int32_t)a - (int32_t)rq.x - HYOBFS_SALT_LEN;
+            const bool in = c < tc && rq.y != 0;
+            const bool pad = in && p >= (int32_t)HYOBFS_GECKO_HEADER_LEN && p + 16 <= hp;
+            const bool msg = in && p >= hp && p + 16 <= pl;
+            S.kind[u] = pad ? 1 : msg ? 2 : 0;
+            const uint64_t co = (uint64_t)rq.w << 32 | rq.z;
+            S.kq[u] = q;
+            S.v[u] = gk_load16u(msg ? B.msg + co + (uint32_t)(p - hp) : safe);
+        }
+    };
+#else
     auto issue = [&](uint32_t T, Step& S) {
 #pragma unroll
         for (int u = 0; u < kGkU; ++u) {
@@ -338,6 +387,24 @@ __device__ __forceinline__ void gecko_encode_aligned(const KeyParams& K, const h
             S.v[u] = gk_load16u(src);
         }
     };
+#endif
+#if HY_GK_MERGE
+    auto retire = [&](uint32_t T, Step& S) {
+#pragma unroll
+        for (int u = 0; u < kGkU; ++u) {
+            if (__ballot(S.kind[u] == 1)) {   // the whole wave: a quad computes one 64-byte block
+                const uint32_t c = T + lane + 64 * u;
+                const gk_u128 ks = gk_ks_quad(P, (base + 16ull * c) >> 6, lane & 3u);
+                S.v[u] = S.kind[u] == 1 ? ks : S.v[u];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < kGkU; ++u) {
+            const uint32_t c = T + lane + 64 * u;
+            if (S.kind[u]) store16_stream(ob + 16 * c, S.v[u] ^ G.key[2 * S.kq[u] + (c & 1)]);
+        }
+    };
+#else
     auto retire = [&](uint32_t T, const Step& S) {
 #pragma unroll
         for (int u = 0; u < kGkU; ++u) {
@@ -354,6 +421,7 @@ __device__ __forceinline__ void gecko_encode_aligned(const KeyParams& K, const h
             if (S.kind[u] == 2) store16_stream(ob + 16 * c, S.v[u] ^ G.key[2 * S.kq[u] + (c & 1)]);
         }
     };
+#endif
     constexpr uint32_t STEP = 64 * kGkU;
 #if HY_GK_PIPE
     // Software pipelined: iteration i+1's loads are issued before iteration i's
@@ -425,7 +493,11 @@ __global__ __launch_bounds__(256) HY_GK_ATTR void gecko_encode_kernel(KeyParams 
             salt = B.salts[f];
             // keyLocked (salamander.go:88-91) in registers; the hash overlaps other waves' sweeps
             uint64_t kw[4];
+#if HY_GK_ABL & 1
+            kw[0] = salt, kw[1] = ~salt, kw[2] = salt * 3, kw[3] = salt ^ 0x55;
+#else
             wave_key<SW>(K, salt, kw);
+#endif
             k0 = (gk_u128)kw[1] << 64 | kw[0];
             k1 = (gk_u128)kw[3] << 64 | kw[2];
         }
