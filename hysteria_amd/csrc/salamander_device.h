@@ -239,9 +239,20 @@ __device__ __forceinline__ void store_masked(uint8_t* dst, u128 r, uint32_t cov)
 
 // quad_perm DPP move (lane i of each quad reads lane CTRL[i]): the diagonal steps of
 // four-lanes-per-state BLAKE2b (salamander_tile.h) and ChaCha (gecko.hip)
+// update_dpp with bound_ctrl (zero fill; quad_perm never reads out of bounds, so the
+// result is the plain permute): that lets the compiler fold the permute into the VALU
+// instruction that reads it (v_add_u32_dpp, v_xor_b32_dpp) instead of a separate
+// v_mov_b32_dpp -- 207 of the Gecko kernel's 216 such moves (ChaCha diagonals)
+#ifndef HY_DPP_FUSE
+#define HY_DPP_FUSE 1
+#endif
 template <int CTRL>
 __device__ __forceinline__ uint32_t qperm32(uint32_t x) {
+#if HY_DPP_FUSE
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, 0xF, 0xF, true);
+#else
     return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, CTRL, 0xF, 0xF, false);
+#endif
 }
 constexpr int kQRot1 = 0x39;   // quad_perm [1,2,3,0]: lane i reads lane i+1
 constexpr int kQRot2 = 0x4E;   // [2,3,0,1]

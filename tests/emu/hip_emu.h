@@ -171,6 +171,8 @@ inline int hyemu_mov_dpp(int v, int ctrl) {
     return hyemu::xchg(v, (lane & ~3) | ((ctrl >> (2 * (lane & 3))) & 3));
 }
 #define __builtin_amdgcn_mov_dpp(v, ctrl, rm, bm, bc) hyemu_mov_dpp((int)(v), (ctrl))
+// full row/bank masks and quad_perm (no lane out of bounds): `old` is never taken
+#define __builtin_amdgcn_update_dpp(old, v, ctrl, rm, bm, bc) ((void)(old), hyemu_mov_dpp((int)(v), (ctrl)))
 inline uint32_t hyemu_alignbit(uint32_t hi, uint32_t lo, uint32_t s) {
     return (uint32_t)((((uint64_t)hi << 32) | lo) >> (s & 31));
 }
