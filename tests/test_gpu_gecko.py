@@ -244,6 +244,51 @@ def test_encode_kernel_frame_grid(gpu):
         assert body == payload
 
 
+@pytest.mark.parametrize("order", ["ascending", "shuffled"])
+def test_encode_dense_small_frames_with_gaps(gpu, order):
+    """Frames of 14..72 wire bytes (one 16-byte chunk can hold parts of three frames),
+    pad 0..23 and chunk 1..35 bytes taken from anywhere in the message buffer, with
+    random gaps of 0..40 bytes between the wire datagrams.  In ascending wire order the
+    groups take the aligned sweep (frame-record walk, edge chunks merged across frames,
+    padding and message chunks next to gaps); shuffled, the per-frame window path.
+    Every frame's wire equals the oracle's; gap bytes keep their sentinel."""
+    import torch
+    import hysteria_amd
+    from hysteria_amd import gecko
+    rng = np.random.default_rng(11 if order == "ascending" else 12)
+    n = 3000
+    pad, clen = rng.integers(0, 24, n), rng.integers(1, 36, n)
+    coff = rng.integers(0, 4096 - 40, n)
+    tot = rng.integers(2, 9, n)
+    idx = rng.integers(0, 8, n) % tot
+    msg = rng.integers(0, 256, 4096, dtype=np.uint8)
+    fr = np.array([(int(coff[i]), int(clen[i]), int(pad[i]), i & 0xFF, (int(idx[i]) << 4) | int(tot[i]))
+                   for i in range(n)], dtype=gecko.FRAME_DTYPE)
+    wl = (13 + pad + clen).astype(np.uint64)
+    gaps = rng.integers(0, 41, n).astype(np.uint64)
+    off = np.cumsum(np.concatenate([[gaps[0]], wl[:-1] + gaps[1:]])).astype(np.uint64)
+    total = int(off[-1] + wl[-1])
+    if order == "shuffled":
+        perm = rng.permutation(n)
+        fr, off, wl = fr[perm], off[perm], wl[perm]
+    salts = sref.splitmix64_array(33, 0, n)
+    o = hysteria_amd.SalamanderObfuscator(PSK, 0)
+    try:
+        out = torch.full((total + 64,), 0xA5, dtype=torch.uint8, device=gpu)
+        gecko.encode_batch(o, msg=_dev(msg, gpu), frames=_dev(fr, gpu), salts=_dev(salts, gpu), pad_key=KEY,
+                           pad_nonce=NONCE, out=out, out_off=_dev(off, gpu), n=n)
+        got = out.cpu().numpy()
+    finally:
+        o.close()
+    exp = gref.encode_wire(PSK, msg.tobytes(), fr.tolist(), salts, KEY, NONCE, off)
+    covered = np.zeros(total + 64, bool)
+    for k in range(n):
+        a, b = int(off[k]), int(off[k] + wl[k])
+        assert got[a:b].tobytes() == exp[k], (order, k)
+        covered[a:b] = True
+    assert (got[~covered] == 0xA5).all()
+
+
 # TestDecodeFrameRejectsInvalid (gecko_frame_test.go:77-96) through the DEVICE parser.
 # The parser classifies as ReadFrom does (gecko.go:176-193): an empty datagram is
 # skipped before decodeFrame (EMPTY) and a clear top bit is passed through (PASS);
