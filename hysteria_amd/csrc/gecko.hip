@@ -3,18 +3,23 @@
 // Encode: one wavefront per group of 64 frames.  The wire datagram of frame f is
 //     salt(8) || (hdr(5) || pad || chunk) ^ key_f[i % 32]
 // (gecko_frame.go:39-61 encodeFrame, then salamander.go:59-72 Obfuscate).  Lane l
-// loads frame l's record, offsets, salt and key once into LDS (and writes the
-// salt); a wave scan numbers the group's 16-byte plaintext windows, and the 64
-// lanes sweep the interior ones, several per lane in flight (loads first, then
-// stores), each lane walking its window's frame forward through the LDS scan: a window
-// inside the chunk is one unaligned 16-byte load, one inside the padding is one
-// column of a ChaCha8 keystream block (keyed per batch; four lanes per block, see
-// gk_ks_quad), each leaves as one 16-byte store.  Then lane l merges frame l's few edge windows
-// (header, padding/chunk seam, frame end) under byte masks; keeping them out of
-// the sweep keeps its lanes on the same path.  Lane l hashes frame l's key
-// (BLAKE2b-256, wave_key<SW> of salamander_wave.h: one instantiation per salt word)
-// in registers in step 1, so the hash overlaps other waves' sweeps (a separate
-// keys_kernel pass via the workspace was 15 % slower).
+// loads frame l's record, offsets and salt and hashes its key in registers (BLAKE2b-256,
+// wave_key<SW> of salamander_wave.h: one instantiation per salt word), so the hash
+// overlaps other waves' sweeps (a separate keys_kernel pass via the workspace was 15 %
+// slower).  Then, when the group's frames lie in ascending wire order (what
+// plan_fragments / writeFragmented produce), the aligned path:
+//   1. per frame, the key rotated to the wire's 32-byte phase, the salt and a 16-byte
+//      record (wire start, lengths, chunk offset) into LDS; the keystream columns of the
+//      edge chunks that hold padding, a column per lane;
+//   2. lane l stores frame l's edge chunks (salt and header, the padding/chunk seam,
+//      the end), merging every frame that touches such a chunk under byte masks;
+//   3. the 64 lanes sweep the group's wire range in aligned 16-byte chunks, two
+//      iterations of loads in flight, each lane walking its frame record forward: a chunk
+//      inside the padding is one column of a ChaCha8 keystream block (keyed per batch;
+//      four lanes per block, gk_ks_quad), one inside the message bytes one unaligned
+//      load; each leaves XORed with the key as one 16-byte non-temporal store.
+// Otherwise the per-frame window path sweeps 16-byte plaintext windows of each frame
+// (numbered by a wave scan) and finishes the edge windows after the sweep.
 //
 // Parse: one thread per deobfuscated datagram, the checks of ReadFrom
 // (gecko.go:170-193) and decodeFrame (gecko_frame.go:65-86) in their order.
@@ -54,7 +59,7 @@ __device__ __forceinline__ gk_u128 gk_mask(uint32_t lo, uint32_t hi) {   // byte
 #define HY_GK_MERGE 1   // aligned sweep: padding and message chunks leave through one conditional store
 #endif
 #ifndef HY_GK_EDGE_KS
-#define HY_GK_EDGE_KS 1   // edge chunks' padding keystream computed by lane quads up front (not one lane per block)
+#define HY_GK_EDGE_KS 1   // edge chunks' padding keystream computed up front, a column per lane (not inside the edge loop)
 #endif
 constexpr int kGkU = HY_GK_U;   // windows per lane in flight
 
@@ -74,7 +79,7 @@ struct GeckoGroup {             // one wave's 64 frames, in LDS
     gk_u128 key[128];           // the frame's key, two halves (aligned path: rotated to the wire phase)
 #if HY_GK_EDGE_KS
     gk_u128 eks[128];           // aligned path: keystream of frame k's edge chunks holding padding
-                                // ([2k] the pad's first chunk, [2k + 1] its last), four lanes per block
+                                // ([2k] the pad's first chunk, [2k + 1] its last)
 #endif
 };
 
