@@ -47,10 +47,7 @@ __device__ __forceinline__ gk_u128 gk_mask(uint32_t lo, uint32_t hi) {   // byte
 #define HY_GK_PIPE 1   // software-pipelined aligned sweep (two iterations' loads in flight)
 #endif
 #ifndef HY_GK_U
-#define HY_GK_U 3   // with HY_GK_REC, 4 spills at the 5-wave register cap
-#endif
-#ifndef HY_GK_REC
-#define HY_GK_REC 1   // aligned sweep: one 16-byte LDS record per frame (wire start, lengths, chunk offset)
+#define HY_GK_U 3   // 4 spills at the 5-wave register cap
 #endif
 #ifndef HY_GK_ABL
 #define HY_GK_ABL 0   // ablations (wrong output, timing only): 1 no key hash, 2 no edge chunks, 4 no edge keystream
@@ -69,12 +66,11 @@ struct GeckoGroup {             // one wave's 64 frames, in LDS
             uint64_t out_off[64];   // wire datagram start
             uint32_t wstart[65];    // first plaintext window of the frame (exclusive scan), [64] = total
         };
-        uint4 rec[65];          // aligned path (HY_GK_REC): {rs, hp_plain, chunk_off lo, hi}, [64] = sentinel
+        uint4 rec[65];          // aligned path: {rs, hp_plain, chunk_off lo, hi}, [64] = sentinel
     };
     uint64_t chunk_off[64];
-    uint64_t hdr[64];           // the 5 header bytes, little-endian in the low bytes
+    uint16_t hid[64];           // msg_id | idx_total << 8 (the header's varying bytes besides pad_len; gk_hdr)
     uint32_t hp_plain[64];      // chunk start (low 16 bits) | plaintext length (high 16 bits)
-    uint32_t rs[65];            // aligned path: wire start relative to the group base, [64] = end of all
     uint64_t salt[64];          // aligned path: the salts (merged into the edge chunks)
     gk_u128 key[128];           // the frame's key, two halves (aligned path: rotated to the wire phase)
 #if HY_GK_EDGE_KS
@@ -82,6 +78,14 @@ struct GeckoGroup {             // one wave's 64 frames, in LDS
                                 // ([2k] the pad's first chunk, [2k + 1] its last)
 #endif
 };
+
+// The 5 header bytes of frame k, little-endian in the low bytes (encodeFrame,
+// gecko_frame.go:39-61): flag, msg_id, idx << 4 | total, pad_len big-endian.
+__device__ __forceinline__ uint64_t gk_hdr(const GeckoGroup& G, uint32_t k) {
+    const uint32_t id = G.hid[k], pad = (G.hp_plain[k] & 0xffff) - HYOBFS_GECKO_HEADER_LEN;
+    return (uint64_t)HYOBFS_GECKO_FLAG_FRAGMENT | (uint64_t)(id & 0xff) << 8 | (uint64_t)(id >> 8) << 16 |
+           (uint64_t)(pad >> 8) << 24 | (uint64_t)(pad & 0xff) << 32;
+}
 
 // ---- padding keystream (include/hyobfs_gecko.h): ChaCha, 8 rounds, RFC 8439 block
 // (constants, 8 key words, 32-bit counter, 3 nonce words), each 64-byte block's
@@ -188,14 +192,14 @@ __device__ __forceinline__ void gk_contrib(const hyobfs_gecko_batch& B, const Gk
     const uint32_t hpl = G.hp_plain[k];
     if (!hpl) return;
     const int32_t hp = (int32_t)(hpl & 0xffff), plain = (int32_t)(hpl >> 16);
-    const uint32_t rs = G.rs[k];
+    const uint32_t rs = G.rec[k].x;
     const int32_t p0 = (int32_t)a - (int32_t)rs - HYOBFS_SALT_LEN;   // plaintext index of chunk byte 0
     const int32_t xlo = max(p0, 0), xhi = min(p0 + 16, plain);
     if (xlo < xhi) {
         gk_u128 X = 0;
         const int32_t hhi = min(p0 + 16, (int32_t)HYOBFS_GECKO_HEADER_LEN);
         if (xlo < hhi) {   // header
-            const gk_u128 H = (gk_u128)G.hdr[k];
+            const gk_u128 H = (gk_u128)gk_hdr(G, k);
             X |= (p0 <= 0 ? H << (8 * -p0) : H >> (8 * p0)) & gk_mask(xlo - p0, hhi - p0);
         }
         const int32_t plo = max(p0, (int32_t)HYOBFS_GECKO_HEADER_LEN), phi = min(p0 + 16, hp);
@@ -246,16 +250,12 @@ __device__ __forceinline__ void gecko_encode_aligned(const KeyParams& K, const h
     const uint64_t base = uni64(__shfl(oo, (int)__builtin_ctzll(vmask), 64)) & ~255ull;
     const uint32_t rs = valid ? (uint32_t)(oo - base) : (prevE > base ? (uint32_t)(prevE - base) : 0u);
     const uint32_t rend = (uint32_t)(maxE - base);
-    G.rs[lane] = rs;
-    if (lane == 0) G.rs[64] = rend;
     if (!valid) G.hp_plain[lane] = 0;
-#if HY_GK_REC
     {   // (out_off, which this overlays, is not read on the aligned path)
         const uint64_t co = valid ? G.chunk_off[lane] : 0ull;
         G.rec[lane] = make_uint4(rs, valid ? G.hp_plain[lane] : 0u, (uint32_t)co, (uint32_t)(co >> 32));
         if (lane == 0) G.rec[64] = make_uint4(0xFFFFFFFFu, 0u, 0u, 0u);   // stops every walk
     }
-#endif
     if (valid) {   // the key rotated so that rel address (a + b) mod 32 indexes it
         const uint64_t kw[4] = {(uint64_t)k0, (uint64_t)(k0 >> 64), (uint64_t)k1, (uint64_t)(k1 >> 64)};
         uint64_t kr[4];
@@ -299,7 +299,7 @@ __device__ __forceinline__ void gecko_encode_aligned(const KeyParams& K, const h
         const uint32_t hpl = G.hp_plain[q];
         hp = (int32_t)(hpl & 0xffff);
         const int32_t pl = (int32_t)(hpl >> 16);
-        p = (int32_t)a - (int32_t)G.rs[q] - HYOBFS_SALT_LEN;
+        p = (int32_t)a - (int32_t)G.rec[q].x - HYOBFS_SALT_LEN;
         return hpl != 0 && ((p >= (int32_t)HYOBFS_GECKO_HEADER_LEN && p + 16 <= hp) || (p >= hp && p + 16 <= pl));
     };
     // ---- first, the edge chunks of frame `lane` (plain stores, so each such line is
@@ -328,7 +328,7 @@ __device__ __forceinline__ void gecko_encode_aligned(const KeyParams& K, const h
             if (interior(lane, a, p, php)) continue;
             gk_u128 r = 0;
             uint32_t cov = 0;
-            for (uint32_t k = lane; k < 64 && G.rs[k] < a + 16; ++k) gk_contrib(B, P, G, base, k, a, r, cov);
+            for (uint32_t k = lane; k < 64 && G.rec[k].x < a + 16; ++k) gk_contrib(B, P, G, base, k, a, r, cov);
             if (cov == 0xFFFFu) gk_store16u(ob + a, r);   // a plain store: the line stays in L2 for the sweep's part
             else if (cov) store_masked(ob + a, r, cov);
         }
@@ -346,7 +346,6 @@ __device__ __forceinline__ void gecko_encode_aligned(const KeyParams& K, const h
         uint8_t kind[kGkU];   // 0 nothing, 1 padding, 2 message bytes
     };
     uint32_t q = 0;
-#if HY_GK_REC
     // the lane's frame record and the next one's stay in registers: a window moves
     // forward by 64 chunks, so the walk reads one record per frame passed (the sentinel
     // rec[64] stops it) and the classification needs no further LDS read
@@ -373,26 +372,6 @@ __device__ __forceinline__ void gecko_encode_aligned(const KeyParams& K, const h
             S.v[u] = gk_load16u(msg ? B.msg + co + (uint32_t)(p - hp) : safe);
         }
     };
-#else
-    auto issue = [&](uint32_t T, Step& S) {
-#pragma unroll
-        for (int u = 0; u < kGkU; ++u) {
-            const uint32_t c = T + lane + 64 * u, a = 16 * c;
-            S.kind[u] = 0;
-            const uint8_t* src = hy_safe_line();
-            if (c < tc) {
-                while (G.rs[q + 1] <= a) ++q;   // rs[64] = the range end > a stops it
-                int32_t p, hp;
-                if (interior(q, a, p, hp)) {
-                    S.kind[u] = p < hp ? 1 : 2;
-                    if (p >= hp) src = B.msg + G.chunk_off[q] + (p - hp);
-                }
-            }
-            S.kq[u] = q;
-            S.v[u] = gk_load16u(src);
-        }
-    };
-#endif
 #if HY_GK_MERGE
     auto retire = [&](uint32_t T, Step& S) {
 #pragma unroll
@@ -491,9 +470,7 @@ __global__ __launch_bounds__(256) HY_GK_ATTR void gecko_encode_kernel(KeyParams 
             oo = B.out_off[f];
             G.out_off[lane] = oo;
             G.chunk_off[lane] = fr.chunk_off;
-            G.hdr[lane] = (uint64_t)HYOBFS_GECKO_FLAG_FRAGMENT | (uint64_t)fr.msg_id << 8 |
-                          (uint64_t)fr.idx_total << 16 | (uint64_t)(fr.pad_len >> 8) << 24 |
-                          (uint64_t)(fr.pad_len & 0xff) << 32;
+            G.hid[lane] = (uint16_t)(fr.msg_id | fr.idx_total << 8);
             G.hp_plain[lane] = hp | plain << 16;
             salt = B.salts[f];
             // keyLocked (salamander.go:88-91) in registers; the hash overlaps other waves' sweeps
@@ -582,7 +559,7 @@ __global__ __launch_bounds__(256) HY_GK_ATTR void gecko_encode_kernel(KeyParams 
         const uint32_t p = 16 * wi;
         const uint32_t e = min(p + 16, plain);
         gk_u128 v = 0;
-        if (p == 0) v = (gk_u128)G.hdr[k] & gk_mask(0, min(e, (uint32_t)HYOBFS_GECKO_HEADER_LEN));
+        if (p == 0) v = (gk_u128)gk_hdr(G, k) & gk_mask(0, min(e, (uint32_t)HYOBFS_GECKO_HEADER_LEN));
         const uint32_t plo = max(p, (uint32_t)HYOBFS_GECKO_HEADER_LEN), phi = min(e, hp);
         if (plo < phi) v |= pad16(k, p) & gk_mask(plo - p, phi - p);
         const uint32_t clo = max(p, hp);
