@@ -246,16 +246,49 @@ struct hipPointerAttribute_t {
     int isManaged;
     unsigned allocationFlags;
 };
-// emulated host memory is never "mapped": host batches always take the staged pipeline
-inline hipError_t hipPointerGetAttributes(hipPointerAttribute_t*, const void*) { return hipErrorInvalidValue; }
 inline hipError_t hipDeviceSynchronize() { return hipSuccess; }
 inline hipError_t hipMalloc(void** p, size_t n) {
     *p = std::malloc(n ? n : 1);
     return *p ? hipSuccess : hipErrorOutOfMemory;
 }
 inline hipError_t hipFree(void* p) { std::free(p); return hipSuccess; }
-inline hipError_t hipHostMalloc(void** p, size_t n, unsigned) { return hipMalloc(p, n); }
-inline hipError_t hipHostFree(void* p) { return hipFree(p); }
+// hipHostMalloc'd ranges are "mapped" (device pointer = host pointer), as on the GPU:
+// host batches whose arrays all come from hyobfs_host_alloc take the zero-copy path;
+// any other pointer is pageable (hipPointerGetAttributes fails)
+namespace hyemu {
+inline std::mutex& host_mu() { static std::mutex m; return m; }
+inline std::vector<std::pair<uintptr_t, size_t>>& host_ranges() { static std::vector<std::pair<uintptr_t, size_t>> v; return v; }
+}  // namespace hyemu
+inline hipError_t hipHostMalloc(void** p, size_t n, unsigned) {
+    const hipError_t e = hipMalloc(p, n);
+    if (e == hipSuccess) {
+        std::lock_guard<std::mutex> lk(hyemu::host_mu());
+        hyemu::host_ranges().push_back({reinterpret_cast<uintptr_t>(*p), n ? n : 1});
+    }
+    return e;
+}
+inline hipError_t hipHostFree(void* p) {
+    {
+        std::lock_guard<std::mutex> lk(hyemu::host_mu());
+        auto& v = hyemu::host_ranges();
+        for (size_t i = 0; i < v.size(); ++i)
+            if (v[i].first == reinterpret_cast<uintptr_t>(p)) {
+                v.erase(v.begin() + (long)i);
+                break;
+            }
+    }
+    return hipFree(p);
+}
+inline hipError_t hipPointerGetAttributes(hipPointerAttribute_t* a, const void* p) {
+    const uintptr_t x = reinterpret_cast<uintptr_t>(p);
+    std::lock_guard<std::mutex> lk(hyemu::host_mu());
+    for (const auto& r : hyemu::host_ranges())
+        if (x >= r.first && x < r.first + r.second) {
+            *a = hipPointerAttribute_t{hipMemoryTypeHost, 0, const_cast<void*>(p), const_cast<void*>(p), 0, 0};
+            return hipSuccess;
+        }
+    return hipErrorInvalidValue;
+}
 inline hipError_t hipHostGetDevicePointer(void** d, void* h, unsigned) { *d = h; return hipSuccess; }
 inline hipError_t hipMemsetAsync(void* p, int v, size_t n, hipStream_t) { std::memset(p, v, n); return hipSuccess; }
 // stream-ordered pool allocation (launches run synchronously here)

@@ -214,8 +214,12 @@ def case_slotted_far(n, L, stride_mb, obf):
     mm.close()
 
 
-def case_host(n, L, chunk, obf):
-    """Host-resident slotted batch through the three-slot pipeline (chunked)."""
+def case_host(n, L, chunk, obf, mapped=0):
+    """Host-resident slotted batch through the three-slot pipeline (chunked); mapped=1:
+    every array from hyobfs_host_alloc, so the batch runs zero-copy on the mapped
+    memory (one batch call) and bytes outside the datagrams' regions stay untouched."""
+    import ctypes
+    from hysteria_amd import _lib
     rng = np.random.default_rng(n + L)
     stride_in = L + 24
     lens = rng.integers(0, L + 1, n).astype(np.uint32)
@@ -225,6 +229,18 @@ def case_host(n, L, chunk, obf):
     out_stride = L + 8 if obf else L
     out = np.full(n * out_stride, 0xA5, np.uint8)
     out_len = np.zeros(n, np.uint32)
+    held = []
+    if mapped:
+        lib = _lib.load()
+
+        def host(a):   # a copy of array a in mapped pinned memory (hyobfs_host_alloc)
+            ptr = lib.hyobfs_host_alloc(a.nbytes)
+            assert ptr
+            held.append(ptr)
+            m = np.ctypeslib.as_array(ctypes.cast(ptr, ctypes.POINTER(ctypes.c_uint8)), (a.nbytes,)).view(a.dtype)
+            m[:] = a
+            return m
+        inp, lens, salts, out, out_len = host(inp), host(lens), host(salts), host(out), host(out_len)
     o = SalamanderObfuscator(b"average_password", 0)
     if obf:
         o.obfuscate_host(inp, n, in_stride=stride_in, in_len=lens, salts=salts, out=out, out_stride=out_stride,
@@ -241,6 +257,14 @@ def case_host(n, L, chunk, obf):
             exp = ref.deobfuscate(b"average_password", src, out_stride)
         assert int(out_len[i]) == len(exp), (i, int(out_len[i]), len(exp))
         assert out[i * out_stride:i * out_stride + len(exp)].tobytes() == exp, i
+    if mapped:
+        untouched = np.ones(n * out_stride, bool)
+        for i in range(n):
+            untouched[i * out_stride:i * out_stride + int(out_len[i])] = False
+        assert (out[untouched] == 0xA5).all()
+        del inp, lens, salts, out, out_len
+        for ptr in held:
+            lib.hyobfs_host_free(ptr)
 
 
 def case_gecko(n_msgs, seed, layout=0):
@@ -382,7 +406,7 @@ if __name__ == "__main__":
     elif which == "uniform":
         case_uniform(args[0], args[1], bool(args[2]))
     elif which == "host":
-        case_host(args[0], args[1], args[2], bool(args[3]))
+        case_host(args[0], args[1], args[2], bool(args[3]), args[4] if len(args) > 4 else 0)
     elif which == "conn":
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         from conn_cases import run_conn_scenarios

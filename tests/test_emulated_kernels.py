@@ -105,6 +105,8 @@ CASES = [
     ("ragged", "11 1500 40 0 1", "2"),
     ("host", "1000 300 96 1", "2"),      # host-resident batch, chunked pipeline
     ("host", "1000 300 96 0", "2"),
+    ("host", "600 300 0 1 1", "2"),      # every array mapped (hyobfs_host_alloc): the zero-copy batch
+    ("host", "600 300 0 0 1", "2"),
     ("conn", "64 120", "2"),             # UDP loopback through the conn wrapper (conn.go)
     ("coalesce", "8 150 4 32", "2"),     # many threads on one coalescing conn (hyobfs_conn_set_coalescing)
     ("lifecycle", "60 16", "2"),         # close() flushes, wakes blocked callers; deferred send errors
