@@ -24,12 +24,13 @@ on the same kernel sources (sha256 of hysteria_amd/csrc/*, see
 scripts/collect_profiles.sh).  cpu_baseline times the C restatement in oracle/
 (a port: no Go toolchain exists on the box) on host cores.
 
-Leg order: each workload times its deobfuscate pass first and the obfuscate
-pass (the headline) second, each after the same W warm-up steps.  Whatever
-runs in a cold GPU's first ~10 ms of sustained load slows by up to 12 % (a GPU
-power-state transient: per-call kernel traces with either direction first,
-profiles/r05_transient/), so the headline is measured after it, at the rate a
-busy serving GPU sustains; the deobfuscate figure takes the transient.
+Warm load: whatever runs in a cold GPU's first ~10 ms of sustained load slows by
+up to 12 % (a GPU power-state transient: per-call kernel traces with either
+direction first, profiles/r05_transient/).  Each workload therefore first runs a
+fixed warm load -- alternating obfuscate and deobfuscate steps for at least
+WARM_LOAD_MS of wall time -- and then times its deobfuscate pass and its obfuscate
+pass (the headline), each after the same W warm-up steps: both directions are
+measured at the rate a busy serving GPU sustains.
 """
 from __future__ import annotations
 
@@ -51,12 +52,15 @@ PSK = b"average_password"
 METRIC = "device-resident packet-obfs GiB/s @ 1200B datagrams, 1/2/4/8 MI355X"
 # the obfuscate kernel each workload runs, per --kernel (rocprof names in profiles/)
 BIMODAL_MIN_WARMUP = 20
+WARM_LOAD_MS = 60.0   # the fixed warm load before a workload's timed legs (>= 20 ms, see above)
 KERNEL_NAMES = {
     "uniform": {"auto": "salamander_tile_kernel<obfuscate> (salamander_tile.h)",
                 "tile": "salamander_tile_kernel<obfuscate> (salamander_tile.h)",
+                "flat": "salamander_tile_kernel<obfuscate> (salamander_tile.h)",
                 "wave": "salamander_wave_kernel<obfuscate, slotted> (salamander_wave.h)"},
-    "bimodal": {"auto": "salamander_wave_kernel<obfuscate, packed> (salamander_wave.h) + width/length scan (2 launches)",
-                "tile": "salamander_wave_kernel<obfuscate, packed> (salamander_wave.h) + width/length scan (2 launches)",
+    "bimodal": {"auto": "salamander_flat_kernel<obfuscate> (salamander_flat.h) + width/length scan and locate prepass (3 launches)",
+                "tile": "salamander_flat_kernel<obfuscate> (salamander_flat.h) + width/length scan and locate prepass (3 launches)",
+                "flat": "salamander_flat_kernel<obfuscate> (salamander_flat.h) + width/length scan and locate prepass (3 launches)",
                 "wave": "salamander_wave_kernel<obfuscate, packed> (salamander_wave.h) + width/length scan (2 launches)"},
 }
 
@@ -73,7 +77,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--no-bimodal", action="store_true", help="N=1: skip the configs[2] sub-object")
-    ap.add_argument("--kernel", choices=["auto", "wave", "tile"], default="auto")
+    ap.add_argument("--kernel", choices=["auto", "wave", "tile", "flat"], default="auto")
+    ap.add_argument("--warm-load-ms", type=float, default=WARM_LOAD_MS)
     return ap.parse_args()
 
 
@@ -312,11 +317,22 @@ def main():
         mine = time.perf_counter() - t0
         return allmax(mine), mine, ev0.elapsed_time(ev1) / 1e3 / steps
 
+    def warm_load(w):
+        """The fixed warm load ("Warm load" above): obfuscate + deobfuscate steps for at
+        least --warm-load-ms of wall time, synchronised every 8 pairs."""
+        t0 = time.perf_counter()
+        while (time.perf_counter() - t0) * 1e3 < args.warm_load_ms:
+            for _ in range(8):
+                w["obf"]()
+                w["deobf"]()
+            torch.cuda.synchronize()
+
     def measure(w, workload, warmup):
-        """Timed deobfuscate and obfuscate passes of one workload: the line's fields
-        (deobfuscate first: see "Leg order" above).  The deobfuscate pass reads the wire
-        the warm-up obfuscate step wrote."""
+        """Timed deobfuscate and obfuscate passes of one workload, after the warm load:
+        the line's fields.  The deobfuscate pass reads the wire the warm-up obfuscate
+        steps wrote."""
         w["obf"]()
+        warm_load(w)
         wall_deobf, _, ev_deobf = timed(w["deobf"], args.steps, warmup)
         wall_obf, mine_obf, ev_obf = timed(w["obf"], args.steps, warmup)
         total_payload = w["payload"] * world * args.steps   # every step processes the whole batch
@@ -379,6 +395,7 @@ def main():
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
+        "warm_load_ms": args.warm_load_ms,
         "ms_per_step": round(m["ms"], 4),
         "higher_is_better": True,
         "scaling": "weak",

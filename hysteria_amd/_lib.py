@@ -21,7 +21,7 @@ HYOBFS_ERR_NOMEM = -4
 HYOBFS_ERR_NO_DEVICE = -5
 HYOBFS_ERR_IO = -6
 HYOBFS_ERR_CLOSED = -7
-ABI_VERSION = 3   # the HYOBFS_ABI_VERSION these bindings are written for (include/hyobfs.h)
+ABI_VERSION = 4   # the HYOBFS_ABI_VERSION these bindings are written for (include/hyobfs.h)
 
 
 class HyobfsBatch(ctypes.Structure):

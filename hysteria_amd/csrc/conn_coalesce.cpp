@@ -181,7 +181,7 @@ struct Coalescer {
     std::deque<int> ready, freelist;
     int rx_err = 0;                      // transient receive error, reported once
     int rx_fatal = 0;                    // the socket is unusable (EBADF, ENOTSOCK, ...): every later read
-    std::atomic<uint64_t> received{0}, rx_batches{0}, rx_dropped{0};
+    std::atomic<uint64_t> received{0}, rx_batches{0}, rx_dropped{0}, rx_gpu_errors{0};
     std::thread reader;
     std::atomic<int> callers{0};         // threads inside coalescer_read / coalescer_write
     bool stopped = false;
@@ -340,18 +340,25 @@ void Coalescer::submit_rx(int i, uint32_t k) {
     received += (uint64_t)k;
 }
 
-// Waits for batch i's kernel and queues it for ReadFrom.
+// Waits for batch i's kernel and queues it for ReadFrom.  A batch whose GPU step
+// failed is not "invalid packets" (the reference drops only datagrams Deobfuscate
+// rejects, conn.go:81-86): its datagrams are lost, the batch goes back to the free
+// list, and ReadFrom reports EIO once (rx_err), as WriteTo does for the send side.
 void Coalescer::finish_rx(int i) {
     Batch& b = rx[i];
     if (b.gpu_ok && zerocopy_on()) b.gpu_ok = gpu_queue_wait(gq_rx, i) == HYOBFS_OK;
-    if (!b.gpu_ok)
-        for (uint32_t j = 0; j < b.k; ++j) b.b.olen[j] = 0;   // nothing deobfuscated: every datagram dropped
-    ++rx_batches;
     {
         std::lock_guard<std::mutex> lk(rx_mu);
-        b.next = 0;
-        b.done.store(0, std::memory_order_relaxed);
-        ready.push_back(i);
+        if (!b.gpu_ok) {
+            rx_gpu_errors += b.k;
+            rx_err = EIO;
+            freelist.push_back(i);
+        } else {
+            ++rx_batches;
+            b.next = 0;
+            b.done.store(0, std::memory_order_relaxed);
+            ready.push_back(i);
+        }
     }
     cv_ready.notify_all();
 }
@@ -362,6 +369,12 @@ void Coalescer::read_loop() {
         int bi;
         {
             std::unique_lock<std::mutex> lk(rx_mu);
+            if (prev >= 0 && freelist.empty()) {   // no free batch: the launched one goes to readers
+                lk.unlock();                       // first, never waiting on their progress
+                finish_rx(prev);
+                prev = -1;
+                lk.lock();
+            }
             cv_free.wait(lk, [&] { return stop.load() || !freelist.empty(); });
             if (stop) break;
             bi = freelist.front();

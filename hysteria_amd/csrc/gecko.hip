@@ -49,9 +49,6 @@ __device__ __forceinline__ gk_u128 gk_mask(uint32_t lo, uint32_t hi) {   // byte
 #ifndef HY_GK_U
 #define HY_GK_U 3   // 4 spills at the 5-wave register cap
 #endif
-#ifndef HY_GK_ABL
-#define HY_GK_ABL 0   // ablations (wrong output, timing only): 1 no key hash, 2 no edge chunks, 4 no edge keystream
-#endif
 #ifndef HY_GK_MERGE
 #define HY_GK_MERGE 1   // aligned sweep: padding and message chunks leave through one conditional store
 #endif
@@ -94,9 +91,7 @@ __device__ __forceinline__ uint64_t gk_hdr(const GeckoGroup& G, uint32_t k) {
 // The block index is 64-bit: its low word is the counter, its high word is XORed
 // into nonce word 0, so offsets past 256 GiB never repeat a block.
 // Column order lets four lanes compute one block, a column each, with no transpose.
-#ifndef HY_GK_PAD_ROUNDS
-#define HY_GK_PAD_ROUNDS 8
-#endif
+constexpr int kGkPadRounds = 8;   // ChaCha8: part of the wire format (include/hyobfs_gecko.h)
 struct GkPad {
     uint32_t k[8], n[3];
 };
@@ -133,7 +128,7 @@ __device__ __forceinline__ gk_u128 gk_ks_quad(const GkPad& P, uint64_t blk, uint
     const uint32_t d0 = gk_sel4((uint32_t)blk, P.n[0] ^ (uint32_t)(blk >> 32), P.n[1], P.n[2], qi);
     uint32_t a = a0, b = b0, c = c0, d = d0;
 #pragma unroll
-    for (int r = 0; r < HY_GK_PAD_ROUNDS / 2; ++r) {
+    for (int r = 0; r < kGkPadRounds / 2; ++r) {
         GK_QR(a, b, c, d);   // column round
         b = qperm32<kQRot1>(b);
         c = qperm32<kQRot2>(c);
@@ -154,7 +149,7 @@ __device__ __forceinline__ gk_u128 gk_ks_single(const GkPad& P, uint64_t blk, ui
 #pragma unroll
     for (int i = 0; i < 16; ++i) s[i] = x[i];
 #pragma unroll
-    for (int r = 0; r < HY_GK_PAD_ROUNDS / 2; ++r) {
+    for (int r = 0; r < kGkPadRounds / 2; ++r) {
         GK_QR(x[0], x[4], x[8], x[12]);
         GK_QR(x[1], x[5], x[9], x[13]);
         GK_QR(x[2], x[6], x[10], x[14]);
@@ -281,7 +276,7 @@ __device__ __forceinline__ void gecko_encode_aligned(const KeyParams& K, const h
                 if (c1 != c0 && (pe & 15u)) need1 = c1;
             }
         }
-        const unsigned long long any = (HY_GK_ABL & 4) ? 0ull : __ballot(need0 != ~0u || need1 != ~0u);
+        const unsigned long long any = __ballot(need0 != ~0u || need1 != ~0u);
         const uint32_t last = any ? 63u - (uint32_t)__builtin_clzll(any) : 0u;   // last frame with a need
         for (uint32_t j = 0; any && j * 32u <= last; ++j) {   // pass j: needs 64 j .. 64 j + 63 (frames 32 j ..)
             const uint32_t n = j * 64u + lane, fr = n >> 1;
@@ -306,7 +301,7 @@ __device__ __forceinline__ void gecko_encode_aligned(const KeyParams& K, const h
     // still in the L2 when the sweep's streaming stores complete it): the first two (salt, header), the one holding
     // the padding/chunk seam, the last; a chunk an earlier frame reaches into is that
     // frame's, and its owner merges every frame that touches it
-    if (valid && !(HY_GK_ABL & 2)) {
+    if (valid) {
         const uint32_t hp = G.hp_plain[lane] & 0xffff;
         const uint32_t cs = rs >> 4, ce = (rs + HYOBFS_SALT_LEN + plain - 1) >> 4;
         const uint32_t seam = (rs + HYOBFS_SALT_LEN + hp - 1) >> 4;
@@ -475,11 +470,7 @@ __global__ __launch_bounds__(256) HY_GK_ATTR void gecko_encode_kernel(KeyParams 
             salt = B.salts[f];
             // keyLocked (salamander.go:88-91) in registers; the hash overlaps other waves' sweeps
             uint64_t kw[4];
-#if HY_GK_ABL & 1
-            kw[0] = salt, kw[1] = ~salt, kw[2] = salt * 3, kw[3] = salt ^ 0x55;
-#else
             wave_key<SW>(K, salt, kw);
-#endif
             k0 = (gk_u128)kw[1] << 64 | kw[0];
             k1 = (gk_u128)kw[3] << 64 | kw[2];
         }

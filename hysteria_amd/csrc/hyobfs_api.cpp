@@ -621,7 +621,7 @@ void hyobfs_salamander_free(hyobfs_salamander* c) { hyobfs::ctx_release(c); }
 int hyobfs_salamander_device(const hyobfs_salamander* c) { return c ? c->device : -1; }
 
 int hyobfs_salamander_set_kernel(hyobfs_salamander* c, int kernel) {
-    if (!c || kernel < HYOBFS_KERNEL_AUTO || kernel > HYOBFS_KERNEL_TILE) return HYOBFS_ERR_INVALID;
+    if (!c || kernel < HYOBFS_KERNEL_AUTO || kernel > HYOBFS_KERNEL_FLAT) return HYOBFS_ERR_INVALID;
     c->kernel.store(kernel, std::memory_order_relaxed);
     return HYOBFS_OK;
 }
@@ -711,7 +711,7 @@ uint64_t hyobfs_batch_workspace_bytes(const hyobfs_batch* b) {
     bp.out_stride = b->out_stride;
     // the largest need over the kernel choices: independent of the context's
     uint64_t m = 0;
-    for (int k : {hyobfs::kKernelAuto, hyobfs::kKernelWave}) {
+    for (int k : {hyobfs::kKernelAuto, hyobfs::kKernelWave, hyobfs::kKernelFlat}) {
         bp.kernel = k;
         const uint64_t v = hyobfs::batch_workspace_bytes(true, bp);
         m = v > m ? v : m;

@@ -32,7 +32,7 @@ constexpr int kTile = 256;          // datagrams per tile-sum entry of the packe
 constexpr uint32_t kMaxDatagram = (1u << 24) - 64;  // longest datagram a batch accepts
 constexpr uint64_t kMaxStride = 1ull << 24;         // longest slot of a slotted output
 // batch kernels (include/hyobfs.h HYOBFS_KERNEL_*)
-constexpr int kKernelAuto = 0, kKernelWave = 1, kKernelTile = 2;
+constexpr int kKernelAuto = 0, kKernelWave = 1, kKernelTile = 2, kKernelFlat = 3;
 
 // BLAKE2b state for the per-packet key, precomputed on the host from the PSK
 // alone (salamander.go:88-91 hashes PSK || salt; every block before the one
@@ -78,7 +78,7 @@ struct BatchParams {
 // HYOBFS_KERNEL environment variable, else 0)
 int resolve_kernel(int ctx_kernel);
 hipError_t launch_salamander(bool obfuscate, const BatchParams& b, const KeyParams& k, hipStream_t s);
-// the kernel launch_salamander would run (kKernelTile / kKernelWave;
+// the kernel launch_salamander would run (kKernelTile / kKernelWave / kKernelFlat;
 // kKernelAuto for an empty batch)
 int batch_kernel(bool obfuscate, const BatchParams& b);
 // device scratch a launch of this batch needs (0: none); launch_salamander takes it

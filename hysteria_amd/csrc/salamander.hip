@@ -7,13 +7,15 @@
 //   Deobfuscate: out[i] = in[8 + i] ^ key[i % 32], reject len <= 8  (:74-86)
 //   key = BLAKE2b-256(PSK || salt)                              (:88-91)
 //
-// Two batch kernels ("Kernels"), both HBM-bound byte work, no MFMA:
+// Three batch kernels ("Kernels"), all HBM-bound byte work, no MFMA:
 //   * salamander_tile_kernel (salamander_tile.h): slotted batches whose region
 //     edges are all multiples of 8 -- the uniform 1200-byte headline batch.
 //     One-shot workgroups of 16 datagrams: a key wave beside three data waves.
+//   * salamander_flat_kernel (salamander_flat.h): contiguous input into packed
+//     output (configs[2]).  One-shot workgroups per 16 KiB of output.
 //   * salamander_wave_kernel (salamander_wave.h): every other layout (packed
 //     output, ragged lengths, any alignment).  One wave per 64-datagram group.
-#include "salamander_tile.h"
+#include "salamander_group.h"
 
 namespace hyobfs {
 
@@ -26,7 +28,13 @@ namespace hyobfs {
     extern template void launch_tile_sw<true, n>(const BatchParams&, const KeyParams&, const TileParams&,   \
                                                  hipStream_t);                                              \
     extern template void launch_tile_sw<false, n>(const BatchParams&, const KeyParams&, const TileParams&,  \
-                                                  hipStream_t);
+                                                  hipStream_t);                                             \
+    extern template void launch_flat_sw<true, n>(const BatchParams&, const KeyParams&, const FlatParams&,   \
+                                                 hipStream_t);                                              \
+    extern template void launch_flat_sw<false, n>(const BatchParams&, const KeyParams&, const FlatParams&,  \
+                                                  hipStream_t);                                             \
+    extern template void launch_group_sw<true, n>(const BatchParams&, const KeyParams&, uint64_t, hipStream_t); \
+    extern template void launch_group_sw<false, n>(const BatchParams&, const KeyParams&, uint64_t, hipStream_t);
 HY_EXTERN_SW(0) HY_EXTERN_SW(1) HY_EXTERN_SW(2) HY_EXTERN_SW(3) HY_EXTERN_SW(4) HY_EXTERN_SW(5)
 HY_EXTERN_SW(6) HY_EXTERN_SW(7) HY_EXTERN_SW(8) HY_EXTERN_SW(9) HY_EXTERN_SW(10) HY_EXTERN_SW(11)
 HY_EXTERN_SW(12) HY_EXTERN_SW(13) HY_EXTERN_SW(14) HY_EXTERN_SW(15)
@@ -67,7 +75,8 @@ __global__ __launch_bounds__(256) void tile_sums_kernel(BatchParams B, uint64_t 
 // block sequentially.  (Loading each thread's 16 consecutive values directly --
 // one cache line per lane -- took 20 us per array for 16384 tiles on the one CU
 // that runs this; this takes 12.)
-__global__ __launch_bounds__(1024) void scan_tiles_kernel(uint64_t* v, uint64_t* v2, uint64_t ntiles) {
+__global__ __launch_bounds__(1024) void scan_tiles_kernel(uint64_t* v, uint64_t* v2, uint64_t ntiles,
+                                                         uint64_t* init2 = nullptr) {
     constexpr int PER = 8, BLK = 64 * PER;
     constexpr int PAD = PER + 1;             // LDS row of a lane: PER values + 1 (fewer bank conflicts)
     __shared__ uint64_t s_x[16][64 * PAD];   // per wave: its block, lane-major
@@ -76,6 +85,7 @@ __global__ __launch_bounds__(1024) void scan_tiles_kernel(uint64_t* v, uint64_t*
     uint64_t* const arr = blockIdx.x ? v2 : v;
     const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
     if (t == 0) s_carry = 0;
+    if (init2 && blockIdx.x == 0 && t < 2) init2[t] = ~0ull;   // the flat prepass's cut record (salamander_flat.h)
     __syncthreads();
     for (uint64_t base = 0; base < ntiles; base += 16 * BLK) {
         const uint64_t wb = base + (uint64_t)wid * BLK;
@@ -196,14 +206,16 @@ __global__ void synth_bimodal_kernel(uint32_t* dst, uint64_t n, uint64_t seed, u
 // ------------------------------------------------------------------ launchers
 
 // Kernel choice ("Kernels"): AUTO runs the tile kernel where it
-// applies (tile_params) and the wave kernel elsewhere; WAVE forces the wave
-// kernel; TILE is AUTO.  HYOBFS_KERNEL=wave|tile sets what AUTO means in a process.
+// applies (tile_params), the flat kernel on contiguous input into packed output
+// (flat_eligible) and the wave kernel elsewhere; WAVE forces the wave kernel; TILE
+// and FLAT are AUTO.  HYOBFS_KERNEL=wave|tile|flat sets what AUTO means in a process.
 static int kernel_override() {   // HYOBFS_KERNEL, as HYOBFS_KERNEL_* (0 = auto); read once, thread-safe
     static const int v = [] {
         const char* e = std::getenv("HYOBFS_KERNEL");
         return !e                        ? kKernelAuto
                : std::strcmp(e, "wave") == 0 ? kKernelWave
                : std::strcmp(e, "tile") == 0 ? kKernelTile
+               : std::strcmp(e, "flat") == 0 ? kKernelFlat
                                              : kKernelAuto;
     }();
     return v;
@@ -241,23 +253,30 @@ static void launch_main(const BatchParams& bp, const KeyParams& k, hipStream_t s
 // (tile_sums_kernel, scan_tiles_kernel).  Otherwise (slotted output, shorter packed
 // runs) a prepass writes the input offsets into the scratch -- length sums, their
 // scan, in_offsets_kernel -- and the kernels for explicit offsets run on them.
+static bool flat_eligible(const BatchParams& b) {   // the flat kernel (salamander_flat.h)
+    return contiguous_input(b) && b.out_stride == 0 && resolve_kernel(b.kernel) != kKernelWave &&
+           (reinterpret_cast<uintptr_t>(b.in) & 15u) == 0;
+}
 static bool wave_scans_input(const BatchParams& b) {   // the wave kernel scans the lengths itself
-    return contiguous_input(b) && b.out_stride == 0 && wave_packed_run_log2() == 6;
+    return contiguous_input(b) && b.out_stride == 0 && !flat_eligible(b) && wave_packed_run_log2() == 6;
 }
 
-// scratch: [width sums | length sums] (ntiles + 1 each), then, when the prepass
-// writes them, the input offsets (8 B per datagram)
+// scratch: [width sums | length sums] (ntiles + 1 each), then the flat prepass's
+// header and tile descriptors, or (when the prepass writes them) the input offsets
+// (8 B per datagram)
 uint64_t batch_workspace_bytes(bool obf, const BatchParams& b) {
     (void)obf;
     if (b.n == 0) return 0;
     const uint64_t tsums = (div_up(b.n, kTile) + 1) * 8;
     if (!contiguous_input(b)) return b.out_stride == 0 ? tsums : 0;
+    if (flat_eligible(b)) return 2 * tsums + flat_workspace_bytes(b.out_cap);
     return 2 * tsums + (wave_scans_input(b) ? 0 : 8 * b.n);
 }
 
 // Which kernel launch_salamander runs for this batch (HYOBFS_KERNEL_*; no launch).
 int batch_kernel(bool obf, const BatchParams& b) {
     if (b.n == 0) return kKernelAuto;   // nothing runs
+    if (flat_eligible(b)) return kKernelFlat;
     TileParams T;
     BatchParams bp = b;
     if (contiguous_input(b) && !wave_scans_input(b))
@@ -268,11 +287,54 @@ int batch_kernel(bool obf, const BatchParams& b) {
 }
 
 template <bool OBF>
-static hipError_t launch_contiguous(BatchParams& bp, hipStream_t s) {
+static hipError_t launch_contiguous(BatchParams& bp, const KeyParams& k, hipStream_t s, bool& done) {
+    done = false;
     if (!bp.scratch) return hipErrorInvalidValue;
     const uint64_t ntiles = div_up(bp.n, kTile);
     bp.tile_sums = static_cast<uint64_t*>(bp.scratch);
     bp.in_tile_sums = bp.tile_sums + ntiles + 1;
+    if (flat_eligible(bp) && resolve_kernel(bp.kernel) != kKernelFlat) {   // sums, their scan, the group kernel
+        const dim3 grid((uint32_t)div_up(ntiles, 4)), block(256);
+        hipLaunchKernelGGL(tile_sums_kernel<OBF>, grid, block, 0, s, bp, ntiles);
+        hipLaunchKernelGGL(scan_tiles_kernel, dim3(2), dim3(1024), 0, s, bp.tile_sums, bp.in_tile_sums, ntiles);
+        bp.tile_prefix = bp.tile_sums;
+        bp.in_tile_prefix = bp.in_tile_sums;
+        switch (k.salt_pos >> 3) {
+#define HY_CASE(n) \
+    case n: launch_group_sw<OBF, n>(bp, k, ntiles, s); break;
+            HY_CASE(0) HY_CASE(1) HY_CASE(2) HY_CASE(3) HY_CASE(4) HY_CASE(5) HY_CASE(6) HY_CASE(7)
+            HY_CASE(8) HY_CASE(9) HY_CASE(10) HY_CASE(11) HY_CASE(12) HY_CASE(13) HY_CASE(14)
+            HY_CASE(15)
+#undef HY_CASE
+        }
+        done = true;
+        return hipGetLastError();
+    }
+    if (flat_eligible(bp)) {   // sums, their scan, the locate prepass, the flat kernel
+        FlatParams F;
+        F.cut = bp.in_tile_sums + ntiles + 1;
+        F.desc = reinterpret_cast<FlatDesc*>(F.cut + 2);
+        F.out_total = bp.tile_sums + ntiles;     // the width scan's total
+        F.in_total = bp.in_tile_sums + ntiles;   // the length scan's total
+        F.ntiles_max = flat_ntiles_max(bp.out_cap);
+        F.t0 = 0;
+        const dim3 grid((uint32_t)div_up(ntiles, 4)), block(256);
+        hipLaunchKernelGGL(tile_sums_kernel<OBF>, grid, block, 0, s, bp, ntiles);
+        hipLaunchKernelGGL(scan_tiles_kernel, dim3(2), dim3(1024), 0, s, bp.tile_sums, bp.in_tile_sums, ntiles, F.cut);
+        bp.tile_prefix = bp.tile_sums;
+        bp.in_tile_prefix = bp.in_tile_sums;
+        hipLaunchKernelGGL(flat_locate_kernel<OBF>, grid, block, 0, s, bp, F, ntiles);
+        switch (k.salt_pos >> 3) {
+#define HY_CASE(n) \
+    case n: launch_flat_sw<OBF, n>(bp, k, F, s); break;
+            HY_CASE(0) HY_CASE(1) HY_CASE(2) HY_CASE(3) HY_CASE(4) HY_CASE(5) HY_CASE(6) HY_CASE(7)
+            HY_CASE(8) HY_CASE(9) HY_CASE(10) HY_CASE(11) HY_CASE(12) HY_CASE(13) HY_CASE(14)
+            HY_CASE(15)
+#undef HY_CASE
+        }
+        done = true;
+        return hipGetLastError();
+    }
     if (wave_scans_input(bp)) return hipSuccess;   // the packed launch below scans both sums
     uint64_t* in_off = bp.in_tile_sums + ntiles + 1;
     const dim3 grid((uint32_t)div_up(ntiles, 4)), block(256);
@@ -293,8 +355,9 @@ hipError_t launch_salamander(bool obf, const BatchParams& b, const KeyParams& k,
     if (k.nblk == 2 && (k.salt_pos >> 3) != 15) return hipErrorInvalidValue;   // by construction
     BatchParams bp = b;
     if (contiguous_input(b)) {
-        const hipError_t e = obf ? launch_contiguous<true>(bp, s) : launch_contiguous<false>(bp, s);
-        if (e != hipSuccess) return e;
+        bool done = false;
+        const hipError_t e = obf ? launch_contiguous<true>(bp, k, s, done) : launch_contiguous<false>(bp, k, s, done);
+        if (e != hipSuccess || done) return e;
     }
     if (bp.out_stride == 0) {
         if (!bp.tile_sums) return hipErrorInvalidValue;

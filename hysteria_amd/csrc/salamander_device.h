@@ -193,9 +193,25 @@ __device__ __forceinline__ uint64_t wave_incl_scan(uint64_t x, int lane) {
     }
     return x;
 }
+__device__ __forceinline__ uint32_t wave_incl_scan32(uint32_t x, int lane) {
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(x, d, 64);
+        if (lane >= d) x += y;
+    }
+    return x;
+}
 __device__ __forceinline__ uint64_t wave_sum(uint64_t x) {
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d, 64);
+    return x;
+}
+__device__ __forceinline__ uint64_t wave_max_u64(uint64_t x) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        const uint64_t y = __shfl_xor(x, d, 64);
+        x = x > y ? x : y;
+    }
     return x;
 }
 __device__ __forceinline__ uint32_t wave_max(uint32_t x) {

@@ -1,0 +1,442 @@
+// salamander_flat.h -- the flat kernel: CONTIGUOUS input (datagram i at
+// in + in_len[0] + ... + in_len[i-1], include/hyobfs.h) into PACKED output (gfx950).
+// The layout of BASELINE configs[2] and of any batch a reader fills back to back.
+//
+// Reference: extras/obfs/salamander.go:59-91 (Obfuscate, Deobfuscate, keyLocked).
+//
+// The output is cut into tiles of kFT bytes (16 KiB), each written by one one-shot
+// workgroup, so every 128-byte line leaves whole from one workgroup.  With contiguous
+// input the payload bytes behind a tile are one contiguous input window, known from
+// the tile's first datagram alone:
+//   prepass: width and length sums per 256 datagrams and their scan (shared with the
+//     wave kernel, salamander.hip), then flat_locate_kernel: per datagram its output
+//     offset and width (the reference's return values, out_off / out_len) and, for
+//     every tile whose first byte it holds, the tile's descriptor (the datagram, its
+//     output and input offsets);
+//   flat kernel, one workgroup of four waves per tile:
+//     1. every wave issues its rows of the window's LDS-DMA (global_load_lds_dwordx4,
+//        non-temporal, 1 KiB per wave instruction) first, so the copy is in flight
+//        during everything else;
+//     2. every wave loads the lengths and salts of the tile's datagrams (lane per
+//        datagram) and scans them (32-bit, tile-relative); wave w hashes the keys of
+//        datagrams 16w .. 16w + 15 four lanes per key (quad_key, salamander_tile.h),
+//        rotated to the output's 32-byte phase; wave 0 writes the table;
+//     3. one barrier, then every thread composes four 16-byte output chunks:
+//        * inside one payload (the common case): two 8-byte LDS reads of the stage --
+//          with contiguous input the stage offset of a datagram's payload is a
+//          multiple of 8 away from its output offset -- XOR one 16-byte key read;
+//        * across one region edge (a datagram's end, the next one's salt and start):
+//          the two datagrams' stage reads, keys and salts, merged per 8-byte half by
+//          three byte boundaries with bit-field selects (v_bfi_b32);
+//        * anything else (three or more datagrams in a chunk, payload bytes outside
+//          the window or off the 8-byte grid): a byte-masked merge that may read
+//          global memory -- correct for every batch, rare for real traffic;
+//        and stores each with one non-temporal 16-byte store (the batch's last chunk
+//        byte-masked).
+// A tile reached by more than kFD datagrams takes several passes of 2-3; a chunk two
+// passes share gets each pass's bytes by a byte-masked store.  Applies to contiguous input with packed
+// output and 16-byte aligned `in` and `out` (flat_eligible, salamander.hip); the wave
+// kernel takes every other packed layout.
+#pragma once
+#include "salamander_tile.h"
+
+namespace hyobfs {
+
+#ifndef HY_FLAT_T
+#define HY_FLAT_T 16384
+#endif
+constexpr uint32_t kFT = HY_FLAT_T;   // output bytes per tile
+static_assert(kFT % 4096 == 0 && kFT <= 65536, "a tile is four 16-byte chunks per thread");
+constexpr uint32_t kFThreads = kFT / 64;   // threads per workgroup: four output chunks each
+constexpr uint32_t kFWaves = kFThreads / 64;
+constexpr int kFU = 4;                     // output chunks per thread
+constexpr int kFD = 64;                  // datagrams per pass (a lane each)
+constexpr uint32_t kFGuard = 32;         // LDS bytes on both sides of the stage (reads of masked bytes)
+// staged input bytes: a tile's payload bytes (obfuscate: at most kFT), plus the wire
+// salts between them (deobfuscate: 8 per datagram of a pass), plus 16-byte rounding
+template <bool OBF>
+constexpr uint32_t flat_stage_bytes() { return kFT + (OBF ? 32u : 8u * kFD + 32u); }
+#ifndef HY_FLAT_MIN_WAVES
+#define HY_FLAT_MIN_WAVES 8
+#endif
+#ifndef HY_FLAT_PRIO
+#define HY_FLAT_PRIO 0   // wave priority while hashing (s_setprio), 0 = none
+#endif
+#ifndef HY_FLAT_LAUNCH_TILES
+#define HY_FLAT_LAUNCH_TILES 0   // tiles per launch (0: one launch)
+#endif
+// w[] flag bits above the width (widths are < 2^24)
+constexpr uint32_t kFlatOffWin = 1u << 31;   // some payload byte of the tile lies outside the staged window
+constexpr uint32_t kFlatOffGrid = 1u << 30;  // stage offset not a multiple of 8 from the output offset
+constexpr uint32_t kFlatWMask = kFlatOffGrid - 1u;
+
+struct FlatDesc {       // one output tile: the first valid datagram reaching into it
+    uint64_t d;         // its index
+    uint64_t o;         // its output offset
+    uint64_t i;         // its input offset
+};
+
+struct FlatParams {
+    FlatDesc* desc;     // ntiles_max + 1 entries
+    // the first datagram that does not fit out_cap (written by the one wave holding
+    // it, ~0 = none): [0] its output offset = the end of the valid output, [1] its index
+    uint64_t* cut;
+    uint64_t ntiles_max;
+    const uint64_t* in_total;    // input bytes: the length scan's total (device)
+    const uint64_t* out_total;   // the width scan's total: the valid output's end without a cut
+    uint64_t t0;        // first tile of this launch
+};
+
+inline uint64_t flat_ntiles_max(uint64_t out_cap) { return (out_cap + kFT - 1) / kFT; }
+// the prepass's scratch: two header words, the descriptor of every tile out_cap allows
+inline uint64_t flat_workspace_bytes(uint64_t out_cap) { return 16 + sizeof(FlatDesc) * (flat_ntiles_max(out_cap) + 1); }
+
+// Per datagram: width (drop rules), output and input offsets from the scans, the
+// reference's return values, and the descriptor of every tile whose first byte the
+// datagram holds.  One wave per 256-datagram tile of the scan, four datagrams per lane.
+// The valid output ends at the first datagram with a width that does not fit out_cap
+// (every later one is dropped too); exactly one wave holds it -- the one whose first
+// datagram's offset still fits -- and records it with plain stores.
+template <bool OBF>
+__global__ __launch_bounds__(256) void flat_locate_kernel(BatchParams B, FlatParams F, uint64_t ntiles) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t tile = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (tile >= ntiles) return;   // whole waves
+    const uint64_t p0 = tile * kTile + 4ull * lane;
+    uint32_t L[4], W[4];
+    uint64_t sl = 0, sw = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        L[k] = p0 + k < B.n ? B.in_len[p0 + k] : 0u;
+        W[k] = p0 + k < B.n ? out_width<OBF>(L[k], B.pkt_cap) : 0u;
+        sl += L[k];
+        sw += W[k];
+    }
+    const uint64_t wave_o = B.tile_prefix[tile];   // every earlier datagram with a width fits iff <= out_cap
+    uint64_t o = wave_o + wave_incl_scan(sw, (int)lane) - sw;
+    uint64_t i = B.in_tile_prefix[tile] + wave_incl_scan(sl, (int)lane) - sl;
+    uint64_t cut = ~0ull;   // index of this lane's first datagram that does not fit
+    uint64_t cut_o = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint64_t p = p0 + k;
+        if (p < B.n) {
+            const bool fits = W[k] && o + W[k] <= B.out_cap;   // else dropped; offsets never move
+            if (B.out_off) B.out_off[p] = o;
+            if (B.out_len) B.out_len[p] = fits ? W[k] : 0u;
+            if (fits) {
+                for (uint64_t t = (o + kFT - 1) / kFT; t * kFT < o + W[k]; ++t) F.desc[t] = FlatDesc{p, o, i};
+            } else if (W[k] && cut == ~0ull) {
+                cut = p;
+                cut_o = o;
+            }
+        }
+        o += W[k];
+        i += L[k];
+    }
+    // the first cut in this wave; the batch's first if everything before the wave fit
+    const unsigned long long m = __ballot(cut != ~0ull);
+    if (m && wave_o <= B.out_cap) {
+        const int l0 = __builtin_ctzll(m);
+        const uint64_t c = __shfl(cut, l0, 64), co = __shfl(cut_o, l0, 64);
+        if (lane == 0) {
+            F.cut[0] = co;
+            F.cut[1] = c;
+        }
+    }
+}
+
+template <bool OBF>
+struct FlatLDS {
+    uint8_t stage[kFGuard + flat_stage_bytes<OBF>() + kFGuard];   // input window, byte 0 at stage[kFGuard]
+    uint64_t key[kFD][4];     // key rotated to the output's 32-byte phase
+    uint64_t salt[kFD];
+    int32_t o[kFD + 1];       // output start relative to the tile ([m..] = INT_MAX)
+    int32_t dlt[kFD];         // stage index of the payload byte at tile-relative output x: x + dlt
+    uint32_t w[kFD];          // width (0: dropped) | kFlatOffWin | kFlatOffGrid
+};
+
+// The helpers below take any LDS layout with the fields of FlatLDS (stage with kFGuard
+// bytes on both sides, key, salt, o, dlt, w): the flat kernel's and the group kernel's
+// (salamander_group.h).
+// 16 bytes of the stage from stage index q (>= -kFGuard, < stage bytes + kFGuard - 16)
+template <class LDS>
+__device__ __forceinline__ u128 flat_stage16(const LDS& S, int32_t q) {
+    const int32_t a = q + (int32_t)kFGuard;
+    const int32_t b = a & ~15;
+    const uint32_t sh = (uint32_t)(a & 15);
+    const u128 A = *reinterpret_cast<const u128*>(S.stage + b);
+    const u128 C = *reinterpret_cast<const u128*>(S.stage + b + 16);
+    return sh ? (A >> (8 * sh)) | (C << (128 - 8 * sh)) : A;
+}
+
+// Payload bytes [base, base + 16) of the datagram whose PL payload bytes start at
+// input position ip, of which the caller keeps [.., need) (the rest is masked): from
+// the stage when the window holds the kept bytes, else one in-bounds global load.
+template <class LDS>
+__device__ __forceinline__ u128 flat_payload16(const LDS& S, const uint8_t* __restrict__ in, uint64_t ws,
+                                               uint32_t wlen, uint64_t ip, uint32_t PL, int32_t base, int32_t need) {
+    const int64_t pos = (int64_t)ip + base;
+    if (pos >= (int64_t)ws - 16 && pos + need <= (int64_t)(ws + wlen)) return flat_stage16(S, (int32_t)(pos - (int64_t)ws));
+    const uint8_t* src = in + ip;
+    if (PL >= 16) {
+        const int32_t w = min(max(base, 0), (int32_t)PL - 16);
+        const u128 V = load16u(src + w);
+        const int32_t d = w - base;
+        return d >= 0 ? (V << (8 * d)) : (V >> (8 * -d));
+    }
+    u128 X = 0;
+    for (int32_t j = max(base, 0); j < min(base + 16, (int32_t)PL); ++j) X |= (u128)src[j] << (8 * (j - base));
+    return X;
+}
+
+// Everything datagram k of the table contributes to the chunk at tile-relative rel
+// (the general merge: any alignment, any number of datagrams per chunk); kh = the
+// chunk's key half (its output offset / 16, mod 2).
+template <bool OBF, class LDS>
+__device__ __forceinline__ void flat_contrib(const LDS& S, const uint8_t* __restrict__ in, uint64_t ws,
+                                             uint32_t wlen, uint32_t k, int32_t rel, uint32_t kh, u128& r, uint32_t& cov) {
+    constexpr int32_t SALT = OBF ? 8 : 0;
+    const uint32_t W = S.w[k] & kFlatWMask;
+    const int32_t o = S.o[k];
+    if (W == 0 || o >= rel + 16 || o + (int32_t)W <= rel) return;
+    if (OBF) {   // salt bytes [o, o + 8)
+        const int32_t sb = max(o, rel), se = min(o + 8, rel + 16);
+        if (sb < se) {
+            u128 Sv = (u128)S.salt[k];
+            Sv = o >= rel ? (Sv << (8 * (o - rel))) : (Sv >> (8 * (rel - o)));
+            r |= Sv & bytemask((uint32_t)(sb - rel), (uint32_t)(se - rel));
+            cov |= ((1u << (se - sb)) - 1u) << (sb - rel);
+        }
+    }
+    const int32_t ps = max(o + SALT, rel), pe = min(o + (int32_t)W, rel + 16);
+    if (ps < pe) {
+        // the payload's input position: stage index of payload byte 0, back to input
+        const uint64_t ip = (uint64_t)((int64_t)ws + (int64_t)(o + SALT) + S.dlt[k]);
+        const u128 X = flat_payload16(S, in, ws, wlen, ip, W - (uint32_t)SALT, rel - (o + SALT), pe - rel);
+        const uint64_t* kw = S.key[k] + 2 * kh;
+        const u128 K = (u128)kw[1] << 64 | kw[0];
+        r |= (X ^ K) & bytemask((uint32_t)(ps - rel), (uint32_t)(pe - rel));
+        cov |= ((1u << (pe - ps)) - 1u) << (ps - rel);
+    }
+}
+
+// Bytes [0, b) of an 8-byte half (b clamped to 0..8), as a 64-bit mask.
+__device__ __forceinline__ uint64_t flat_lomask(int32_t b) {
+    const uint32_t c = (uint32_t)min(max(b, 0), 8);
+    return c ? ~0ull >> (64u - 8u * c) : 0ull;
+}
+// (m & x) | (~m & y) per bit: v_bfi_b32 on each half
+__device__ __forceinline__ uint64_t flat_bfi(uint64_t m, uint64_t x, uint64_t y) { return (m & x) | (~m & y); }
+
+// One 16-byte output chunk at tile-relative rel from the table of m datagrams (ND
+// entries, o[ND] a sentinel), kh = 2 x its key half: true with the value when the chunk
+// lies inside one payload, or across one region edge (q's salt or end, then at most the
+// datagram after it) with both datagrams staged on the 8-byte grid; false when it needs
+// the general merge.
+template <bool OBF, int ND, class LDS>
+__device__ __forceinline__ bool flat_chunk(const LDS& S, int32_t rel, uint32_t kh, uint32_t m, u128& value) {
+    constexpr int32_t SALT = OBF ? 8 : 0;
+    uint32_t q = 0;   // last datagram whose output starts at or before rel
+#pragma unroll
+    for (uint32_t s = ND / 2; s; s >>= 1) q = S.o[q + s] <= rel ? q + s : q;
+    const int32_t oq = S.o[q];
+    const uint32_t wq = S.w[q];
+    const int32_t eq = oq + (int32_t)(wq & kFlatWMask);   // q's region end
+    // q's region holds byte 0; at most q+1 (starting right at q's end, staged, on the
+    // grid) holds the rest
+    const uint32_t q1 = q + 1;
+    const int32_t o1 = S.o[q1];   // == eq unless q is the last of the pass
+    const uint32_t w1 = q1 < m ? S.w[q1] : 0u;
+    const int32_t e1 = o1 + (int32_t)(w1 & kFlatWMask);
+    const bool fast = oq <= rel && (wq & (kFlatOffWin | kFlatOffGrid)) == 0 && eq > rel &&
+                      (eq >= rel + 16 || (o1 == eq && (w1 & (kFlatOffWin | kFlatOffGrid)) == 0 && e1 >= rel + 16));
+    if (!fast) return false;
+    const uint64_t* dq = reinterpret_cast<const uint64_t*>(S.stage + (rel + S.dlt[q] + (int32_t)kFGuard));
+    const uint64_t xl = dq[0] ^ S.key[q][kh], xh = dq[1] ^ S.key[q][kh + 1];
+    if (oq + SALT <= rel && rel + 16 <= eq) {   // inside q's payload
+        value = (u128)xh << 64 | xl;
+        return true;
+    }
+    // q's salt [oq, oq + 8), q's payload [oq + 8, eq), q+1's salt [eq, eq + 8),
+    // q+1's payload: byte boundaries b1 <= b2 <= b3, chunk-relative
+    uint64_t lo = 0, hi = 0;
+    const int32_t b1 = oq + SALT - rel, b2 = eq - rel, b3 = b2 + SALT;
+    if (eq < rel + 16) {   // q+1 starts in this chunk (b2 in 1..15)
+        const uint64_t* d1 = reinterpret_cast<const uint64_t*>(S.stage + (rel + S.dlt[q1] + (int32_t)kFGuard));
+        lo = d1[0] ^ S.key[q1][kh];
+        hi = d1[1] ^ S.key[q1][kh + 1];
+        if (OBF) {   // q+1's salt at byte b2
+            const uint64_t s1 = S.salt[q1];
+            const uint32_t e8 = 8u * (uint32_t)b2;
+            const uint64_t s1l = e8 < 64 ? s1 << e8 : 0ull;
+            const uint64_t s1h = e8 < 64 ? s1 >> (64 - e8) : s1 << (e8 - 64);
+            lo = flat_bfi(flat_lomask(b3), s1l, lo);
+            hi = flat_bfi(flat_lomask(b3 - 8), s1h, hi);
+        }
+    }
+    lo = flat_bfi(flat_lomask(b2), xl, lo);
+    hi = flat_bfi(flat_lomask(b2 - 8), xh, hi);
+    if (OBF) {   // q's salt ends at byte b1 <= 8: low half only
+        const uint32_t c8 = 8u * (uint32_t)min(rel - oq, 8);
+        const uint64_t sq = c8 < 64 ? S.salt[q] >> c8 : 0ull;
+        lo = flat_bfi(flat_lomask(b1), sq, lo);
+    }
+    value = (u128)hi << 64 | lo;
+    return true;
+}
+
+template <bool OBF, int SW>
+__global__ __launch_bounds__(kFThreads, HY_FLAT_MIN_WAVES) void salamander_flat_kernel(BatchParams B, KeyParams K,
+                                                                                  FlatParams F) {
+    constexpr int32_t SALT = OBF ? 8 : 0;   // salt bytes in front of the output payload
+    constexpr uint32_t SKIP = OBF ? 0u : 8u;   // salt bytes in front of the input payload
+    __shared__ __attribute__((aligned(16))) FlatLDS<OBF> S;
+    const uint32_t wid = uni32(threadIdx.x >> 6);
+    const uint8_t* __restrict__ in = B.in;
+    const uint64_t t = F.t0 + blockIdx.x;
+    const uint64_t E = uni64(min<uint64_t>(F.cut[0], *F.out_total));   // end of the valid output
+    if (t == 0 && threadIdx.x == 0 && B.out_total) atomicAdd(B.out_total, (unsigned long long)E);
+    const uint64_t tT = t * kFT;
+    if (tT >= E) return;   // past the valid output (whole workgroup)
+    const int32_t tl = (int32_t)min<uint64_t>(kFT, E - tT);   // the tile's bytes
+    const FlatDesc D0 = F.desc[t];
+    const uint64_t d0 = uni64(D0.d), o0 = uni64(D0.o), i0 = uni64(D0.i);
+    // the tile's datagrams [d0, dend): the next tile's first one may start in this one
+    const uint64_t dend = uni64(tT + kFT < E ? F.desc[t + 1].d + 1 : min<uint64_t>(F.cut[1], B.n));
+
+    // ---- 1. the input window: from the payload byte behind output byte tT (16-aligned
+    // down), cut at the input's end (a partial last 16 bytes by single lanes)
+    const int64_t first = (int64_t)tT - (int64_t)o0 - SALT;   // payload index of byte tT in d0
+    const uint64_t ws = (i0 + SKIP + (uint64_t)max<int64_t>(first, 0)) & ~15ull;
+    const uint64_t in_total = uni64(*F.in_total);
+    const uint32_t wlen = (uint32_t)min<uint64_t>(flat_stage_bytes<OBF>(), in_total > ws ? in_total - ws : 0);
+    {
+        const uint32_t lane = threadIdx.x & 63;
+        const uint32_t nfull = wlen >> 4;
+        for (uint32_t c = wid; c * 64u < nfull; c += kFWaves) {
+            const uint32_t ch = c * 64u + lane;
+            if (ch < nfull) glds16(in + ws + 16ull * ch, S.stage + kFGuard + 1024u * c);
+        }
+        const uint32_t tail = wlen & 15u;
+        if (tail && wid == kFWaves - 1 && lane < tail) S.stage[kFGuard + 16u * nfull + lane] = in[ws + 16ull * nfull + lane];
+    }
+
+    uint8_t* __restrict__ ob = B.out + tT;
+    uint64_t og = o0, ig = i0;   // offsets of the pass's first datagram
+    for (uint64_t g0 = d0; g0 < dend; g0 += kFD) {
+        const uint32_t m = (uint32_t)min<uint64_t>((uint64_t)kFD, dend - g0);
+        // the thread index made opaque per pass: values derived from it (the quad's
+        // BLAKE2b selects, chunk addresses) are recomputed in each pass, not hoisted out
+        // of the (almost always single-trip) loop and spilled
+        uint32_t tid = threadIdx.x;
+#ifndef HYOBFS_EMULATE
+        asm volatile("" : "+v"(tid));
+#endif
+        const uint32_t lane = tid & 63;
+        // ---- 2. every wave: the pass's lengths, widths, offsets and salts (lane l: datagram g0 + l)
+        const bool live = lane < m;
+        const uint64_t p = g0 + lane;
+        const uint32_t L = live ? B.in_len[p] : 0u;
+        uint64_t salt = live && OBF ? B.salts[p] : 0ull;
+        uint32_t W = live ? out_width<OBF>(L, B.pkt_cap) : 0u;
+        // tile-relative 32-bit scans: a pass spans at most 64 x 2^24 bytes
+        const uint32_t iw = wave_incl_scan32(W, (int)lane);
+        const uint32_t il = wave_incl_scan32(L, (int)lane);
+        const uint64_t o = og + iw - W, i = ig + il - L;
+        og += uni32((uint32_t)__shfl(iw, 63, 64));
+        ig += uni32((uint32_t)__shfl(il, 63, 64));
+        if (W && o + W > B.out_cap) W = 0;   // past out_cap: dropped (not in [d0, dend) unless cut)
+        if (!OBF && W) salt = load8u(in + i);   // the wire's salt
+        const int32_t orel = (int32_t)((int64_t)o - (int64_t)tT);
+        const int32_t dlt = (int32_t)((int64_t)(i + SKIP) - (int64_t)ws) - (orel + SALT);
+        // ---- keys: wave w hashes datagrams 16w .. 16w + 15, four lanes each, rotated
+        // to the output's 32-byte phase (byte x of the row: key byte x - (o + SALT) mod 32)
+        if (16u * wid < m) {
+            const uint32_t k = 16u * wid + (lane >> 2), qi = lane & 3u;
+            const uint64_t sk = __shfl(salt, (int)k, 64);
+            const uint32_t ok = (uint32_t)__shfl((uint32_t)o, (int)k, 64);
+#if HY_FLAT_PRIO && !defined(HYOBFS_EMULATE)
+            __builtin_amdgcn_s_setprio(HY_FLAT_PRIO);   // the hash is the tile's latency chain
+#endif
+            const uint64_t kw = quad_key<SW>(K, sk, qi);
+#if HY_FLAT_PRIO && !defined(HYOBFS_EMULATE)
+            __builtin_amdgcn_s_setprio(0);
+#endif
+            const uint32_t rr = (ok + (uint32_t)SALT) & 31u;
+            const uint32_t st = (8u * qi - rr) & 31u, w0 = st >> 3, sh = (st & 7u) * 8u;
+            const uint64_t a = __shfl(kw, (int)((lane & ~3u) | w0), 64);
+            const uint64_t b = __shfl(kw, (int)((lane & ~3u) | ((w0 + 1) & 3u)), 64);
+            if (k < m) S.key[k][qi] = sh ? (a >> sh) | (b << (64 - sh)) : a;
+        }
+        if (wid == 0) {
+            // the tile's part of the payload inside the staged window, on the 8-byte grid
+            uint32_t fl = 0;
+            if (W) {
+                const int32_t ps = max(orel + SALT, 0), pe = min(orel + (int32_t)W, (int32_t)kFT);
+                if (ps < pe && (ps + dlt < 0 || pe + dlt > (int32_t)wlen)) fl |= kFlatOffWin;
+                if (dlt & 7) fl |= kFlatOffGrid;
+            }
+            S.o[lane] = live ? orel : 0x7FFFFFFF;
+            if (lane == 0) S.o[kFD] = 0x7FFFFFFF;
+            S.w[lane] = W | fl;
+            S.dlt[lane] = dlt;
+            S.salt[lane] = salt;
+        }
+        __syncthreads();   // the stage has landed (every wave's vmcnt(0)), the table and keys are published
+
+        // ---- 3. compose: the chunks inside one payload or across one region edge
+        // first, stored together; the rest (gen) by the general merge afterwards, one at
+        // a time (its registers are not live beside the four values)
+        u128 r[kFU];
+        uint32_t gen = 0;   // bit u: chunk u takes the general merge
+#pragma unroll
+        for (int u = 0; u < kFU; ++u) {
+            const int32_t rel = 16 * (int32_t)(u * kFThreads + tid);
+            r[u] = 0;
+            if (rel >= tl) continue;
+            if (!flat_chunk<OBF, kFD>(S, rel, 2u * (((uint32_t)rel >> 4) & 1u), m, r[u])) gen |= 1u << u;
+        }
+        // ---- store: one non-temporal 16-byte store per chunk, all values finished first
+#pragma unroll
+        for (int u = 0; u < kFU; ++u) {
+            const int32_t rel = 16 * (int32_t)(u * kFThreads + tid);
+            if (rel < tl && !((gen >> u) & 1u)) store16_stream(ob + rel, r[u]);
+        }
+        // ---- the general merge: this pass's datagrams' bytes of the chunk; a chunk it
+        // covers in part (the output's last chunk, a chunk shared with the next pass)
+        // byte-masked
+        while (gen) {
+            const int u = __builtin_ctz(gen);
+            gen &= gen - 1;
+            const int32_t rel = 16 * (int32_t)(u * kFThreads + tid);
+            uint32_t q = 0;
+            for (uint32_t s = kFD / 2; s; s >>= 1) q = S.o[q + s] <= rel ? q + s : q;
+            u128 v = 0;
+            uint32_t cov = 0;
+            for (uint32_t k = q; k < m && S.o[k] < rel + 16; ++k)
+                flat_contrib<OBF>(S, in, ws, wlen, k, rel, ((uint32_t)rel >> 4) & 1u, v, cov);
+            if (cov == 0xFFFFu)
+                store16_stream(ob + rel, v);
+            else if (cov)
+                store_masked(ob + rel, v, cov);
+        }
+        if (g0 + kFD < dend) __syncthreads();   // the next pass overwrites the table and keys
+    }
+}
+
+template <bool OBF, int SW>
+void launch_flat_sw(const BatchParams& b, const KeyParams& k, const FlatParams& F, hipStream_t s) {
+    // one workgroup per tile out_cap allows (those past the valid output exit at once);
+    // at least one, which writes out_total
+    const uint64_t nt = F.ntiles_max < 1 ? 1 : F.ntiles_max;
+    const uint64_t per = HY_FLAT_LAUNCH_TILES ? (uint64_t)HY_FLAT_LAUNCH_TILES : nt;
+    for (uint64_t t0 = 0; t0 < nt; t0 += per) {
+        FlatParams Fl = F;
+        Fl.t0 = t0;
+        const uint64_t g = nt - t0 < per ? nt - t0 : per;
+        hipLaunchKernelGGL((salamander_flat_kernel<OBF, SW>), dim3((uint32_t)g), dim3(kFThreads), 0, s, b, k, Fl);
+    }
+}
+
+}  // namespace hyobfs

@@ -1,6 +1,6 @@
 // salamander_inst.hip -- instantiates the batch kernels for one salt word
 // (compiled once per HY_SW = 0..15, see Makefile).
-#include "salamander_tile.h"
+#include "salamander_group.h"
 
 #ifndef HY_SW
 #error "compile with -DHY_SW=<salt word 0..15>"
@@ -13,4 +13,8 @@ template void launch_wave_sw<false, true, HY_SW>(const BatchParams&, const KeyPa
 template void launch_wave_sw<false, false, HY_SW>(const BatchParams&, const KeyParams&, hipStream_t);
 template void launch_tile_sw<true, HY_SW>(const BatchParams&, const KeyParams&, const TileParams&, hipStream_t);
 template void launch_tile_sw<false, HY_SW>(const BatchParams&, const KeyParams&, const TileParams&, hipStream_t);
+template void launch_flat_sw<true, HY_SW>(const BatchParams&, const KeyParams&, const FlatParams&, hipStream_t);
+template void launch_flat_sw<false, HY_SW>(const BatchParams&, const KeyParams&, const FlatParams&, hipStream_t);
+template void launch_group_sw<true, HY_SW>(const BatchParams&, const KeyParams&, uint64_t, hipStream_t);
+template void launch_group_sw<false, HY_SW>(const BatchParams&, const KeyParams&, uint64_t, hipStream_t);
 }  // namespace hyobfs

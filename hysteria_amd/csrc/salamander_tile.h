@@ -262,14 +262,11 @@ __device__ __forceinline__ void glds16(const uint8_t* g, uint8_t* l) {   // LDS-
 #endif
 }
 
+// Obfuscate: the key wave's early temporal loads of each datagram's input (two per
+// datagram, at payload offsets 0 and ~L/2 rounded down to a line) warm the L2 for the
+// staging DMA (78.8 -> 81.7 %).  HY_TILE_PREFETCH = loads per datagram.
 #ifndef HY_TILE_PREFETCH
 #define HY_TILE_PREFETCH 2
-#endif
-#ifndef HY_TILE_PF_PHASE
-#define HY_TILE_PF_PHASE 0
-#endif
-#ifndef HY_TILE_COMPOSE
-#define HY_TILE_COMPOSE 1
 #endif
 
 // One 8-byte half of an output chunk: datagram q, slot offset rr.  Branch-free:
@@ -293,8 +290,6 @@ __device__ __forceinline__ uint64_t tile_half(const uint8_t* s_in, const uint64_
 template <bool OBF, int SW>
 __global__ __launch_bounds__(256, HY_TILE_MIN_WAVES) void salamander_tile_kernel(BatchParams B, KeyParams K,
                                                                                   TileParams T) {
-    constexpr uint32_t SALT = OBF ? 8u : 0u;   // salt bytes in front of the output payload
-    constexpr uint32_t SKIP = OBF ? 0u : 8u;   // salt bytes in front of the input payload
 #ifdef HYOBFS_EMULATE
     uint8_t* s_in = hyemu_dyn_lds();
 #else
@@ -317,15 +312,15 @@ __global__ __launch_bounds__(256, HY_TILE_MIN_WAVES) void salamander_tile_kernel
         // ---- the key wave: salts, BLAKE2b-256 on quads (lane 4k+i: word i of key k), LDS
         const uint32_t qk = lane >> 2, qi = lane & 3;
         uint64_t salt = 0;
-#ifdef HY_TILE_ABL_SALT
-        salt = p0 + qk;
-#else
         if (qk < nt) salt = OBF ? B.salts[p0 + qk] : load8_wire_salt(ib + qk * in_stride);
-#endif
 #if HY_TILE_PREFETCH
+        // offset qi * in_stride / HY_TILE_PREFETCH, down to a line, and never past the
+        // datagram's own L bytes (the caller promises only those at the last slot)
         uint32_t pf = 0;
-        if (OBF && qk < nt && qi < HY_TILE_PREFETCH)
-            pf = *reinterpret_cast<const uint32_t*>(ib + qk * in_stride + (((2 * qi + HY_TILE_PF_PHASE) * in_stride / (2 * HY_TILE_PREFETCH)) & ~127u));
+        if (OBF && qk < nt && qi < HY_TILE_PREFETCH) {
+            const uint32_t po = min((qi * in_stride / HY_TILE_PREFETCH) & ~127u, (T.LI - 4u) & ~3u);
+            pf = *reinterpret_cast<const uint32_t*>(ib + qk * in_stride + po);
+        }
 #endif
         const uint64_t kw = quad_key<SW>(K, salt, qi);
 #if HY_TILE_PREFETCH && !defined(HYOBFS_EMULATE)
@@ -382,25 +377,9 @@ __global__ __launch_bounds__(256, HY_TILE_MIN_WAVES) void salamander_tile_kernel
                 ++p2;
             }
             const bool vlo = (uint32_t)r < W, vhi = p2 < nt && r2 < W;
-#if HY_TILE_COMPOSE == 1
             st[u] = (vlo ? 1u : 0u) | (vhi ? 2u : 0u);
             lo[u] = tile_half<OBF>(s_in, s_key, s_salt, p, (uint32_t)r, vlo, in_stride);
             hi[u] = tile_half<OBF>(s_in, s_key, s_salt, p2, r2, vhi, in_stride);
-            continue;
-#endif
-            const bool slo = OBF && (uint32_t)r < 8u, shi = OBF && r2 < 8u;
-            const uint32_t jlo = (uint32_t)r - SALT, jhi = r2 - SALT;
-            const uint32_t alo = p * in_stride + SKIP + jlo, ahi = p2 * in_stride + SKIP + jhi;
-            if (vlo && !slo && vhi && !shi && p2 == p) {   // inside one payload: two words, one key pair
-                const uint64_t* d = reinterpret_cast<const uint64_t*>(s_in + alo);
-                const uint32_t ki = p * 8u + ((jlo >> 3) & 3u);
-                lo[u] = d[0] ^ s_key[ki];
-                hi[u] = d[1] ^ s_key[ki + 1];
-            } else {
-                if (vlo) lo[u] = slo ? s_salt[p] : *reinterpret_cast<const uint64_t*>(s_in + alo) ^ s_key[p * 8u + ((jlo >> 3) & 3u)];
-                if (vhi) hi[u] = shi ? s_salt[p2] : *reinterpret_cast<const uint64_t*>(s_in + ahi) ^ s_key[p2 * 8u + ((jhi >> 3) & 3u)];
-            }
-            st[u] = (vlo ? 1u : 0u) | (vhi ? 2u : 0u);
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -448,8 +427,10 @@ inline bool tile_params(const BatchParams& b, TileParams& T) {
 // (profiles/r03_size_probe.txt): within one long launch the XCDs drift apart in the
 // address space, every launch boundary lines them up again.  Launches of 512K
 // datagrams measured another ~0.8 % faster (78.2-78.4 %; 256K 77.5-77.7 %, 128K
-// 74.5-74.7 %: launch gaps); 1M is kept so that the 1M-datagram bench batch stays one
-// launch, whose HIP-event time and rocprofv3 kernel average describe the same thing.
+// 74.5-74.7 %: launch gaps), and 512K is the default.  The 1M-datagram bench batch is
+// therefore two launches: per-call figures sum the launches of one call
+// (scripts/rocprof_per_call.py, scripts/pmc_traffic.py); a rocprofv3 per-kernel average
+// describes half a call.
 #ifndef HY_TILE_LAUNCH_TILES
 #define HY_TILE_LAUNCH_TILES 32768   // 512K datagrams
 #endif

@@ -136,12 +136,12 @@ class SalamanderObfuscator:
     def __exit__(self, *exc):
         self.close()
 
-    KERNELS = {"auto": 0, "wave": 1, "tile": 2}
+    KERNELS = {"auto": 0, "wave": 1, "tile": 2, "flat": 3}
 
     def set_kernel(self, kernel: str) -> None:
-        """Batch kernel of this context: "auto" (the tile kernel where it applies, else the
-        wave-group kernel), "wave" (forced) or "tile" (= auto; include/hyobfs.h,
-        HYOBFS_KERNEL_*)."""
+        """Batch kernel of this context: "auto" (the tile kernel where it applies, the flat
+        kernel on contiguous input into packed output, else the wave-group kernel), "wave"
+        (forced), "tile" or "flat" (= auto; include/hyobfs.h, HYOBFS_KERNEL_*)."""
         check(self._lib.hyobfs_salamander_set_kernel(self._h, self.KERNELS[kernel]), "set_kernel")
         self.kernel = kernel
 
@@ -195,12 +195,12 @@ class SalamanderObfuscator:
         check(f(self._h, ctypes.byref(b), s), "obfuscate_batch" if obf else "deobfuscate_batch")
 
     def batch_kernel(self, obf: bool, *, inp, n, out, **kw) -> str:
-        """The kernel a batch call with these arguments would run ("tile" / "wave"; "none"
+        """The kernel a batch call with these arguments would run ("tile" / "flat" / "wave"; "none"
         for an empty batch): hyobfs_salamander_batch_kernel, no device work."""
         b = _make_batch(inp=inp, n=n, out=out, **kw)
         k = self._lib.hyobfs_salamander_batch_kernel(self._h, ctypes.byref(b), int(bool(obf)))
         check(min(k, 0), "batch_kernel")
-        return {0: "none", 1: "wave", 2: "tile"}[k]
+        return {0: "none", 1: "wave", 2: "tile", 3: "flat"}[k]
 
     @staticmethod
     def workspace_bytes(*, inp, n, out, **kw) -> int:

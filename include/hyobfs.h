@@ -56,7 +56,15 @@
 extern "C" {
 #endif
 
-/* ABI version.  3 (this header) against 2:
+/* ABI version.  4 (this header) against 3:
+ *   - new kernel HYOBFS_KERNEL_FLAT (3): contiguous input into packed output runs
+ *     the flat kernel under AUTO (16-byte aligned in and out); 3 meant STREAM in
+ *     ABI 2 and was rejected in ABI 3;
+ *   - contiguous input with packed output needs more scratch (the flat prepass's
+ *     tile descriptors, 24 B per 16 KiB of out_cap): ask hyobfs_batch_workspace_bytes;
+ *   - hyobfs_conn_free on a connection that was never closed closes its fd (in ABI 2
+ *     it detached and left the socket open; include/hyobfs_conn.h).
+ * 3 against 2:
  *   - HYOBFS_KERNEL_STREAM (3) is gone (the stream kernel lost to the wave-group
  *     kernel on every measured layout); hyobfs_salamander_set_kernel rejects 3;
  *   - hyobfs_gecko_workspace_bytes is gone, and hyobfs_gecko_batch's workspace,
@@ -78,7 +86,7 @@ extern "C" {
  *     pass in_off (all zeros) instead.
  * Bindings compare hyobfs_abi_version() with the version they were written
  * for and refuse a mismatch (hysteria_amd/_lib.py does). */
-#define HYOBFS_ABI_VERSION 3
+#define HYOBFS_ABI_VERSION 4
 
 #define HYOBFS_PSK_MIN_LEN 4  /* smPSKMinLen, salamander.go:14 */
 #define HYOBFS_SALT_LEN 8     /* smSaltLen,   salamander.go:15 */
@@ -126,18 +134,20 @@ int hyobfs_salamander_device(const hyobfs_salamander* ctx);
    HYOBFS_KERNEL_AUTO runs the tile kernel on slotted batches whose region edges
    are all multiples of 8 (one length, slot and input stride multiples of 8,
    payloads of 16 bytes or more, nothing dropped) -- the uniform 1200-byte batch
-   of the benchmark -- and the wave-group kernel on every other batch (packed
-   output, ragged lengths, any alignment; contiguous input scans its lengths
-   alongside the widths).  HYOBFS_KERNEL_WAVE forces the wave-group kernel;
-   HYOBFS_KERNEL_TILE is AUTO.  The HYOBFS_KERNEL environment variable
-   (wave|tile) overrides AUTO.  Returns HYOBFS_ERR_INVALID for an unknown value.
+   of the benchmark --, the flat kernel on contiguous input into packed output
+   (16-byte aligned in; the ragged configs[2] batch), and the wave-group kernel on
+   every other batch (packed output, ragged lengths, any alignment).
+   HYOBFS_KERNEL_WAVE forces the wave-group kernel; HYOBFS_KERNEL_TILE and
+   HYOBFS_KERNEL_FLAT are AUTO.  The HYOBFS_KERNEL environment variable
+   (wave|tile|flat) overrides AUTO.  Returns HYOBFS_ERR_INVALID for an unknown value.
    May be called while other threads run batches on the context (an atomic
    setting; a batch uses the value it read when it started).  Outputs are
    identical. */
 enum {
     HYOBFS_KERNEL_AUTO = 0,
     HYOBFS_KERNEL_WAVE = 1,
-    HYOBFS_KERNEL_TILE = 2
+    HYOBFS_KERNEL_TILE = 2,
+    HYOBFS_KERNEL_FLAT = 3
 };
 int hyobfs_salamander_set_kernel(hyobfs_salamander* ctx, int kernel);
 
@@ -226,12 +236,13 @@ typedef struct hyobfs_batch {
 uint64_t hyobfs_batch_workspace_size(uint64_t n);
 /* Scratch any batch needs, whatever the kernel choice: the above for packed
    batches with explicit offsets; for contiguous input twice that (width and
-   length sums), plus 8 B per datagram (the input offsets a prepass writes) when
-   the output is slotted or HYOBFS_PACKED_RUN_LOG2 shortens the packed runs; 0 for
-   other slotted batches. */
+   length sums), plus, into packed output, 16 B + 24 B per 16 KiB of out_cap (the
+   flat kernel's tile descriptors), or, into slotted output (or with
+   HYOBFS_PACKED_RUN_LOG2 shortening the packed runs), 8 B per datagram (the input
+   offsets a prepass writes); 0 for other slotted batches. */
 uint64_t hyobfs_batch_workspace_bytes(const hyobfs_batch* b);
 /* Which batch kernel a call with this batch would run under the context's
-   setting (HYOBFS_KERNEL_TILE or _WAVE; HYOBFS_KERNEL_AUTO for an
+   setting (HYOBFS_KERNEL_TILE, _FLAT or _WAVE; HYOBFS_KERNEL_AUTO for an
    empty batch), or a negative status for an invalid batch.  No device work:
    tests use it to prove which kernel their case exercised. */
 int hyobfs_salamander_batch_kernel(hyobfs_salamander* ctx, const hyobfs_batch* b, int obfuscate);

@@ -54,7 +54,7 @@ if WL == "bimodal":
     SO = hysteria_amd.SalamanderObfuscator
     nws = max(hysteria_amd.workspace_size(P), SO.workspace_bytes(inp=inp, n=P, in_len=lens, out=wire, out_cap=cap),
               SO.workspace_bytes(inp=wire, n=P, in_len=out_len, out=back, out_cap=total_in))
-    ws = torch.empty(nws, dtype=torch.uint8, device=dev)
+    ws = torch.empty(4 * nws + 40 * P, dtype=torch.uint8, device=dev)   # room for builds with smaller tiles or key arrays
     obf_bytes, deobf_bytes = 2 * total_in + 16 * P, 2 * total_in + 8 * P
     PL = total_in
 else:

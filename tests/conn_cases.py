@@ -353,6 +353,40 @@ def run_lifecycle_scenarios(device: int = 0, n: int = 200, max_batch: int = 64, 
         oa.close()
 
 
+def run_rx_gpu_failure_scenario(device: int = 0, max_batch: int = 16):
+    """A receive batch whose GPU step fails (CPU tier only: tests/emu/hip_emu.h
+    HYEMU_FAIL_EVENTS_FROM=5 fails every wait of the coalescing connection's receive
+    queue).  The reference drops only datagrams Deobfuscate rejects (conn.go:81-86); a
+    device failure is an error, not invalid packets: ReadFrom raises EIO (once per
+    failed batch, after the datagrams queued before it) and rx_dropped stays 0."""
+    import time
+    rng = np.random.default_rng(31)
+    osend, orecv = SalamanderObfuscator(PSK, device), SalamanderObfuscator(PSK, device)
+    raw = _udp()
+    cb = SalamanderPacketConn(_udp(), orecv, batch=max_batch)
+    try:
+        cb.set_coalescing(max_batch, 50)   # its send queue: events 1-4, receive queue: 5-8
+        b_addr = cb.local_addr()
+        for rnd in range(2):
+            for _ in range(3):
+                p = _payload(rng, 100)
+                wire = bytearray(108)
+                assert osend.obfuscate(p, wire, salt=rng.bytes(8)) == 108
+                raw.sendto(bytes(wire), b_addr)
+            time.sleep(0.2)   # one receive batch
+            try:
+                cb.read_from()
+                raise AssertionError("a failed receive batch was not reported")
+            except OSError as e:
+                assert e.errno == errno.EIO, e
+            assert cb.stats()["rx_dropped"] == 0, cb.stats()
+    finally:
+        cb.close()
+        raw.close()
+        osend.close()
+        orecv.close()
+
+
 def _free_unclosed_closes_fd(oa, r_addr, raw, max_batch):
     """hyobfs_conn_wrap on a dup'd descriptor, hyobfs_conn_free with no
     hyobfs_conn_close first (include/hyobfs_conn.h): the fd leaves the process's

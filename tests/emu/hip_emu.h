@@ -231,12 +231,25 @@ inline hipError_t hipOccupancyMaxActiveBlocksPerMultiprocessor(int* nb, K, int, 
 inline hipError_t hipStreamCreateWithFlags(hipStream_t* s, unsigned) { *s = (hipStream_t)1; return hipSuccess; }
 inline hipError_t hipStreamDestroy(hipStream_t) { return hipSuccess; }
 enum { hipEventDisableTiming = 2 };
-inline hipError_t hipEventCreateWithFlags(hipEvent_t* e, unsigned) { *e = (hipEvent_t)1; return hipSuccess; }
+// Events are numbered in creation order (1, 2, ...).  Fault injection for the CPU tier:
+// HYEMU_FAIL_EVENTS_FROM=k makes hipEventSynchronize fail for every event numbered k or
+// later (a coalescing connection's send queue creates events 1-4 and its receive queue
+// 5-8 in a fresh process: k = 5 fails exactly the receive side's GPU steps).
+namespace hyemu {
+inline std::atomic<uintptr_t> g_events{0};
+}
+inline hipError_t hipEventCreateWithFlags(hipEvent_t* e, unsigned) {
+    *e = (hipEvent_t)(hyemu::g_events.fetch_add(1) + 1);
+    return hipSuccess;
+}
 inline hipError_t hipEventDestroy(hipEvent_t) { return hipSuccess; }
 inline hipError_t hipEventRecord(hipEvent_t, hipStream_t) { return hipSuccess; }   // launches run synchronously
 inline hipError_t hipStreamWaitEvent(hipStream_t, hipEvent_t, unsigned) { return hipSuccess; }
 inline hipError_t hipStreamSynchronize(hipStream_t) { return hipSuccess; }
-inline hipError_t hipEventSynchronize(hipEvent_t) { return hipSuccess; }
+inline hipError_t hipEventSynchronize(hipEvent_t e) {
+    static const uintptr_t from = (uintptr_t)hyemu::env_int("HYEMU_FAIL_EVENTS_FROM", 0);
+    return from && (uintptr_t)e >= from ? hipErrorInvalidValue : hipSuccess;
+}
 enum hipMemoryType { hipMemoryTypeUnregistered = 0, hipMemoryTypeHost = 1, hipMemoryTypeDevice = 2 };
 struct hipPointerAttribute_t {
     hipMemoryType type;

@@ -97,9 +97,10 @@ def case_packed_cap(seed, n, maxlen, obf, cap_pct, psk_len):
 
 def case_contig(seed, n, dist, obf, cap_pct, psk_len, pkt_cap=0, misalign=0, out_stride=0):
     """Contiguous input (in_off NULL, in_stride 0: datagram i right after datagram
-    i-1) into packed output (out_stride 0: the wave kernel scans the lengths itself;
-    with HYOBFS_PACKED_RUN_LOG2 < 6 a prepass writes the input offsets) or into slots
-    of out_stride bytes (the prepass's offsets, then the wave kernel).  dist 0: the
+    i-1) into packed output (out_stride 0: the flat kernel under AUTO from 16-byte
+    aligned input; the wave kernel, forced or for misaligned input, scans the lengths
+    itself, and with HYOBFS_PACKED_RUN_LOG2 < 6 a prepass writes the input offsets)
+    or into slots of out_stride bytes (the prepass's offsets, then the wave kernel).  dist 0: the
     bimodal 64/1350 mix; 1: 0..2100 B; 2: 0..40 B (several datagrams per chunk);
     3: 1000..5000 B; 4: bimodal with zero-length ones.  out_cap cut to cap_pct % of
     the full size, pkt_cap drops, deobfuscate of real wire (8-byte wire datagrams
@@ -140,10 +141,17 @@ def case_contig(seed, n, dist, obf, cap_pct, psk_len, pkt_cap=0, misalign=0, out
         assert np.array_equal(woff[1:], np.cumsum(wlen[:-1], dtype=np.uint64))
         inp, in_off, lens, total = winp, woff, np.ascontiguousarray(wlen, np.uint32), wl
     full = n * out_stride if out_stride else total + (8 * n if obf else 0)
+    cap = max(16, full * cap_pct // 100)
     tsums = ((n + 255) // 256 + 1) * 8
+    # packed output from 16-byte aligned input: the flat kernel under AUTO
+    flat = not out_stride and not misalign and os.environ.get("HYOBFS_KERNEL") != "wave"
     prepass = out_stride or os.environ.get("HYOBFS_PACKED_RUN_LOG2", "6") != "6"
-    run(obf, psk, lens, in_off, inp, salts, max(16, full * cap_pct // 100), pkt_cap=pkt_cap, contiguous=True,
-        out_stride=out_stride, expect_kernel="wave", expect_ws=2 * tsums + (8 * n if prepass else 0))
+    # hyobfs_batch_workspace_bytes: the largest need over the kernel choices
+    ws = 2 * tsums + (8 * n if prepass else 0)   # the wave kernel's
+    if not out_stride and not misalign:           # the flat kernel's tile descriptors (16 KiB tiles)
+        ws = max(ws, 2 * tsums + 16 + 24 * ((cap + 16383) // 16384 + 1))
+    run(obf, psk, lens, in_off, inp, salts, cap, pkt_cap=pkt_cap, contiguous=True,
+        out_stride=out_stride, expect_kernel="flat" if flat else "wave", expect_ws=ws)
 
 
 def case_bimodal(n, obf):
@@ -420,6 +428,10 @@ if __name__ == "__main__":
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         from conn_cases import run_lifecycle_scenarios
         run_lifecycle_scenarios(n=args[0], max_batch=args[1])
+    elif which == "rxfail":   # run with HYEMU_FAIL_EVENTS_FROM=5 (tests/emu/hip_emu.h)
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        from conn_cases import run_rx_gpu_failure_scenario
+        run_rx_gpu_failure_scenario()
     elif which == "closerace":
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         from conn_cases import run_close_race_scenarios

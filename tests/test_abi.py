@@ -26,7 +26,7 @@ def test_library_exports_every_header_symbol():
 
 def test_abi_basics():
     lib = _lib.load()
-    assert lib.hyobfs_abi_version() == _lib.ABI_VERSION == 3
+    assert lib.hyobfs_abi_version() == _lib.ABI_VERSION == 4
     assert _lib.status_string(_lib.HYOBFS_ERR_PSK_TOO_SHORT) == "PSK must be at least 4 bytes"
     assert _lib.status_string(_lib.HYOBFS_ERR_CLOSED) == "use of closed connection"
     assert lib.hyobfs_batch_workspace_size(0) == 8

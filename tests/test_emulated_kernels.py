@@ -47,15 +47,17 @@ SPECS = {
     "test_emulated_kernel_vs_oracle": lambda p: (p["which"], p["args"], {"HYEMU_CUS": p["cus"]}),
     "test_emulated_split_launches": lambda p: (p["which"], p["args"], dict(p["env"])),
     "test_emulated_contiguous_input_slotted": lambda p: ("contig", p["args"], {"HYEMU_CUS": "2"}),
+    "test_emulated_rx_gpu_failure_reports_eio": lambda p: ("rxfail", "", {"HYEMU_FAIL_EVENTS_FROM": "5"}),
     "test_emulated_contiguous_input_auto": lambda p: ("contig", p["args"], {"HYEMU_CUS": "2"}),
+    "test_emulated_contiguous_input_wave": lambda p: ("contig", p["args"], {"HYEMU_CUS": "2", "HYOBFS_KERNEL": "wave"}),
     "test_emulated_contiguous_input_prepass_offsets": lambda p: ("contig", p["args"], {
-        "HYEMU_CUS": "2", "HYOBFS_PACKED_RUN_LOG2": "3"}),
+        "HYEMU_CUS": "2", "HYOBFS_PACKED_RUN_LOG2": "3", "HYOBFS_KERNEL": "wave"}),
 }
 
 
 def _spec(item):
     f = SPECS.get(getattr(item, "originalname", None))
-    return f(item.callspec.params) if f else None
+    return f(item.callspec.params if hasattr(item, "callspec") else {}) if f else None
 
 
 def _key(spec):
@@ -152,27 +154,43 @@ PACKED_CASES = [
 
 # Contiguous input (in_off NULL, in_stride 0; tests/emu/run_case.py case_contig:
 # seed n dist obf cap% psk_len [pkt_cap misalign out_stride]).  Packed output under
-# AUTO: the wave kernel taking its input offsets from the scan of the lengths; packed
-# runs of 8 or slotted output: the prepass's input offsets (in_offsets_kernel), then
-# the wave kernel.  Bimodal, 0..2100 B, tiny (several datagrams per chunk), 1-5 KB,
-# zero-length datagrams; out_cap cuts, pkt_cap drops, real wire with 8-byte
-# datagrams, PSKs across salt words and the two-block case, a misaligned input.
+# AUTO: the flat kernel (16 KiB output tiles, salamander_flat.h) from 16-byte aligned
+# input, the wave kernel from misaligned input; forced to the wave kernel: the wave
+# kernel taking its input offsets from the scan of the lengths, or, with packed runs
+# of 8, the prepass's input offsets (in_offsets_kernel).  Bimodal, 0..2100 B, tiny
+# (several datagrams per chunk, tiles of several passes), 1-5 KB, zero-length
+# datagrams; out_cap cuts, pkt_cap drops (dropped input inside a tile's window), real
+# wire with 8-byte datagrams, PSKs across salt words and the two-block case, a
+# misaligned input.  The flat kernel's emulation costs a 256-thread workgroup per
+# 16 KiB of output, so its cases are a few hundred KB.
 CONTIG_CASES = [
     "1 3000 0 1 100 16", "2 3000 0 0 100 16", "3 2000 1 1 100 16", "4 2000 1 0 100 33", "5 3000 2 1 100 16",
     "6 3000 2 0 100 121", "7 300 3 1 100 16", "8 300 3 0 100 4", "9 3000 4 1 100 16", "10 3000 4 0 100 16",
     "11 2000 1 1 60 16", "12 2000 1 0 70 127", "13 2000 1 1 100 16 1000", "14 2000 1 0 100 16 900",
     "15 3000 0 1 100 16 0 1", "16 3000 0 0 100 16 0 1", "17 3000 2 1 50 16",
 ]
+FLAT_CASES = [
+    "1 600 0 1 100 16", "2 600 0 0 100 16", "3 500 1 1 100 16", "4 500 1 0 100 33", "5 3000 2 1 100 16",
+    "6 3000 2 0 100 121", "7 100 3 1 100 16", "8 100 3 0 100 4", "9 600 4 1 100 16", "10 600 4 0 100 16",
+    "11 500 1 1 60 16", "12 500 1 0 70 127", "13 500 1 1 100 16 1000", "14 500 1 0 100 16 900",
+    "15 600 0 1 100 16 0 1", "16 600 0 0 100 16 0 1", "17 3000 2 1 50 16", "18 600 0 1 100 9",
+    "19 600 0 0 100 128",
+]
 
 
-@pytest.mark.parametrize("args", CONTIG_CASES)
+@pytest.mark.parametrize("args", FLAT_CASES)
 def test_emulated_contiguous_input_auto(emu_lib, args):
     _run(emu_lib, "contig", args, {"HYEMU_CUS": "2"})
 
 
+@pytest.mark.parametrize("args", CONTIG_CASES)
+def test_emulated_contiguous_input_wave(emu_lib, args):
+    _run(emu_lib, "contig", args, {"HYEMU_CUS": "2", "HYOBFS_KERNEL": "wave"})
+
+
 @pytest.mark.parametrize("args", [CONTIG_CASES[i] for i in (1, 2, 10)])
 def test_emulated_contiguous_input_prepass_offsets(emu_lib, args):
-    _run(emu_lib, "contig", args, {"HYEMU_CUS": "2", "HYOBFS_PACKED_RUN_LOG2": "3"})
+    _run(emu_lib, "contig", args, {"HYEMU_CUS": "2", "HYOBFS_PACKED_RUN_LOG2": "3", "HYOBFS_KERNEL": "wave"})
 
 
 # Contiguous input into SLOTS (out_stride > 0): the prepass writes the input offsets
@@ -256,3 +274,10 @@ def test_emulated_wave_kernel_forced(emu_lib, which, args, cus):
 @pytest.mark.parametrize("which,args,cus", CASES)
 def test_emulated_kernel_vs_oracle(emu_lib, which, args, cus):
     _run(emu_lib, which, args, {"HYEMU_CUS": cus})
+
+
+def test_emulated_rx_gpu_failure_reports_eio(emu_lib):
+    """A coalescing connection's receive batch whose GPU step fails: ReadFrom raises EIO
+    (once per failed batch) and nothing is counted as an invalid datagram (rx_dropped 0);
+    the emulation fails every wait of the receive queue (HYEMU_FAIL_EVENTS_FROM=5)."""
+    _run(emu_lib, "rxfail", "", {"HYEMU_FAIL_EVENTS_FROM": "5"})

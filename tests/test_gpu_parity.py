@@ -97,15 +97,15 @@ def test_edge_rules_per_packet(obfs):
 
 
 def test_set_kernel_accepts_the_header_values_only(gpu):
-    """hyobfs_salamander_set_kernel: HYOBFS_KERNEL_AUTO..TILE accepted, anything else
-    (3, the removed STREAM, included) HYOBFS_ERR_INVALID (include/hyobfs.h, ABI 3)."""
+    """hyobfs_salamander_set_kernel: HYOBFS_KERNEL_AUTO..FLAT accepted, anything else
+    HYOBFS_ERR_INVALID (include/hyobfs.h, ABI 4)."""
     import hysteria_amd
     from hysteria_amd import _lib
     with hysteria_amd.SalamanderObfuscator(PSK, 0) as o:
         lib = _lib.load()
-        for k in range(3):
+        for k in range(4):
             assert lib.hyobfs_salamander_set_kernel(o._h, k) == 0
-        for k in (-1, 3, 4, 99):
+        for k in (-1, 4, 5, 99):
             assert lib.hyobfs_salamander_set_kernel(o._h, k) == _lib.HYOBFS_ERR_INVALID
 
 
@@ -380,15 +380,22 @@ def test_config3_bimodal_4M_digest(obfs, gpu, golden):
     assert h.hexdigest() == d["obf_sha256"]
 
 
-# ------------------------------------------- contiguous input: the wave kernel's length scan
+# ------------------------------------------- contiguous input: the flat kernel, the wave kernel's length scan
 @pytest.fixture(params=["auto", "wave"])
 def contig_obfs(gpu, request):
-    """auto and wave: the wave kernel scanning the input lengths with the widths."""
+    """auto: the flat kernel into packed output from 16-byte aligned input
+    (salamander_flat.h), else the wave kernel; wave: the wave kernel scanning the input
+    lengths with the widths (packed) or the prepass's input offsets (slotted)."""
     import hysteria_amd
     o = hysteria_amd.SalamanderObfuscator(PSK, 0)
     o.set_kernel(request.param)
     yield o
     o.close()
+
+
+def _contig_kernel(o, packed=True, aligned=True):
+    """The kernel a contiguous-input batch runs under the context's choice."""
+    return "flat" if packed and aligned and o.kernel != "wave" else "wave"
 
 
 def test_contiguous_bimodal_64k_vs_oracle_and_digest(contig_obfs, gpu, coracle, golden):
@@ -407,7 +414,7 @@ def test_contiguous_bimodal_64k_vs_oracle_and_digest(contig_obfs, gpu, coracle, 
     out_len = torch.empty(n, dtype=torch.int32, device=gpu)
     total = torch.zeros(1, dtype=torch.int64, device=gpu)
     kw = dict(in_len=lens, out=out, out_cap=cap, out_off=out_off, out_len=out_len, out_total=total)
-    assert obfs.batch_kernel(True, inp=inp, n=n, salts=salts, **kw) == "wave"
+    assert obfs.batch_kernel(True, inp=inp, n=n, salts=salts, **kw) == _contig_kernel(obfs)
     obfs.obfuscate_batch(inp, n, salts=salts, **kw)
     got = _host(out)
     assert hashlib.sha256(got[:cap].tobytes()).hexdigest() == d["obf_sha256"]
@@ -421,7 +428,7 @@ def test_contiguous_bimodal_64k_vs_oracle_and_digest(contig_obfs, gpu, coracle, 
     assert int(_host(total)[0]) == etot
     back = torch.full((total_in + 64,), 0x5A, dtype=torch.uint8, device=gpu)
     kw = dict(in_len=out_len, out=back, out_cap=total_in, out_total=total)
-    assert obfs.batch_kernel(False, inp=out, n=n, **kw) == "wave"
+    assert obfs.batch_kernel(False, inp=out, n=n, **kw) == _contig_kernel(obfs)
     obfs.deobfuscate_batch(out, n, **kw)
     hb = _host(back)
     assert np.array_equal(hb[:total_in], _host(inp)[:total_in])
@@ -516,11 +523,14 @@ def test_contiguous_input_grid_vs_oracle(contig_obfs, gpu, coracle, case):
     import hysteria_amd
     tsums = ((n + 255) // 256 + 1) * 8
     need = hysteria_amd.SalamanderObfuscator.workspace_bytes(inp=src, n=n, **kw)
-    assert need == 2 * tsums + (8 * n if stride else 0)
+    want = 2 * tsums + (8 * n if stride else 0)
+    if not stride and not mis:   # the flat kernel's tile descriptors (16 KiB tiles)
+        want = max(want, 2 * tsums + 16 + 24 * ((cap + 16383) // 16384 + 1))
+    assert need == want
     ws = torch.full((need + 64,), 0x3C, dtype=torch.uint8, device=gpu)
     with hysteria_amd.SalamanderObfuscator(psk, 0) as o:   # the case's PSK (the fixture's is average_password)
         o.set_kernel(contig_obfs.kernel)
-        assert o.batch_kernel(bool(obf), inp=src, n=n, **kw) == "wave"
+        assert o.batch_kernel(bool(obf), inp=src, n=n, **kw) == _contig_kernel(o, not stride, not mis)
         (o.obfuscate_batch if obf else o.deobfuscate_batch)(inp=src, n=n, workspace=ws, workspace_bytes=need, **kw)
         got = _host(out)
     assert (_host(ws)[need:] == 0x3C).all(), "wrote past the workspace"
