@@ -7,7 +7,9 @@
 // batch:
 //   * send: WriteTo reserves a slot in the filling batch (a short spin lock),
 //     copies the datagram and returns len(p).  A flusher thread seals the batch
-//     when it is full or max_wait_us after its first datagram and launches its
+//     when it is full, max_wait_us after its first datagram, or once no WriteTo
+//     has added to it for idle_us (the writers paused: a light load does not wait
+//     for max_wait; HYOBFS_COALESCE_IDLE_US, default min(20, max_wait_us)), and launches its
 //     obfuscation on the GPU, which reads and writes the batch in place (mapped
 //     pinned memory, gpu_queue_submit); while that kernel runs the thread sends
 //     the PREVIOUS batch with sendmmsg, and the next batch fills.  Three send
@@ -35,6 +37,7 @@
 
 #include <errno.h>
 #include <poll.h>
+#include <sys/prctl.h>
 #include <string.h>
 #include <sys/socket.h>
 #include <sys/time.h>
@@ -95,6 +98,18 @@ static bool zerocopy_on() {
     static const bool v = env_flag("HYOBFS_COALESCE_ZEROCOPY", true);
     return v;
 }
+// Idle seal (HYOBFS_COALESCE_IDLE_US, default 20): a filling batch no WriteTo has added
+// to for this long is sealed without waiting for max_wait_us.  Under load the writers
+// arrive far more often and batches still fill; at a light load a datagram waits about
+// this long instead of max_wait_us.
+static uint32_t coalesce_idle_us() {
+    static const uint32_t v = [] {
+        const char* e = std::getenv("HYOBFS_COALESCE_IDLE_US");
+        const long x = e ? std::atol(e) : 20;
+        return (uint32_t)(x < 0 ? 0 : x);
+    }();
+    return v;
+}
 
 struct Batch {
     Pinned b;
@@ -105,7 +120,7 @@ struct Batch {
     // send side (count / sealed / first under the spin lock)
     uint32_t count = 0;
     bool sealed = false;
-    Clock::time_point first{};
+    Clock::time_point first{}, last{};   // the first and the latest datagram's arrival
     std::atomic<uint32_t> committed{0};
     bool gpu_ok = false;   // its GPU step was launched (or done) without error
     // receive side (k / next under rx_mu)
@@ -160,6 +175,7 @@ struct Coalescer {
     hyobfs_salamander* ctx = nullptr;
     uint32_t max_batch = 0;
     std::chrono::microseconds max_wait{0};
+    std::chrono::microseconds idle{0};   // seal a batch no WriteTo added to for this long
     std::atomic<bool> stop{false};
     GpuQueue* gq_tx = nullptr;           // the send side's stream (gpu_queue_*)
     GpuQueue* gq_rx = nullptr;
@@ -290,13 +306,26 @@ void Coalescer::flush_loop() {
                 if (!pending()) return;   // stopping, nothing left to send
             }
             if (pending()) {
-                spin.lock();
-                const Clock::time_point deadline = tx[cur].first + max_wait;
-                spin.unlock();
-                // nothing on the GPU: wait for the batch to fill or its deadline; a batch on
-                // the GPU: seal this one only if it is due now, else send that one first
-                const bool go = prev < 0 ? (cv_flush.wait_until(lk, deadline, due), true)
-                                         : due() || Clock::now() >= deadline;
+                // due: full, stopping, max_wait after the first datagram, or idle since the
+                // last one.  Nothing on the GPU: sleep until one of those; a batch on the
+                // GPU: seal this one only if it is due now, else send that one first
+                auto wake = [&] {   // the earlier of the deadline and the idle point
+                    spin.lock();
+                    const Clock::time_point d = std::min(tx[cur].first + max_wait, tx[cur].last + idle);
+                    spin.unlock();
+                    return d;
+                };
+                bool go;
+                if (prev < 0) {
+                    for (;;) {
+                        const Clock::time_point w = wake();
+                        if (due() || Clock::now() >= w) break;
+                        cv_flush.wait_until(lk, w, due);
+                    }
+                    go = true;
+                } else {
+                    go = due() || Clock::now() >= wake();
+                }
                 if (go) {   // seal the filling batch; writers move on to the next (already sent)
                     spin.lock();
                     tx[cur].sealed = true;
@@ -454,6 +483,7 @@ Coalescer* coalescer_new(int fd, hyobfs_salamander* ctx, uint32_t max_batch, uin
     q->ctx = ctx;
     q->max_batch = max_batch;
     q->max_wait = std::chrono::microseconds(max_wait_us);
+    q->idle = std::chrono::microseconds(std::min<uint32_t>(max_wait_us, coalesce_idle_us()));
     bool ok = true;
     for (auto& b : q->tx) ok = ok && b.alloc(max_batch);
     for (auto& b : q->rx) ok = ok && b.alloc(max_batch);
@@ -471,7 +501,10 @@ Coalescer* coalescer_new(int fd, hyobfs_salamander* ctx, uint32_t max_batch, uin
         return nullptr;
     }
     for (int i = 0; i < Coalescer::kRx; ++i) q->freelist.push_back(i);
-    q->flusher = std::thread([q] { q->flush_loop(); });
+    q->flusher = std::thread([q] {
+        (void)prctl(PR_SET_TIMERSLACK, 1UL, 0, 0, 0);   // wake at the idle point, not up to 50 us later
+        q->flush_loop();
+    });
     q->reader = std::thread([q] { q->read_loop(); });
     return q;
 }
@@ -550,7 +583,9 @@ int64_t coalescer_write(Coalescer* q, const uint8_t* p, size_t len, const void* 
         b = &q->tx[q->cur];
         if (q->has_space()) {
             idx = b->count++;
-            if (idx == 0) b->first = Clock::now();
+            const Clock::time_point now = Clock::now();
+            if (idx == 0) b->first = now;
+            b->last = now;
             q->spin.unlock();
             break;
         }

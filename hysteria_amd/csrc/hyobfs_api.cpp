@@ -574,6 +574,14 @@ struct GpuQueue {
     hipEvent_t ev[4] = {};
 };
 
+static bool coalesce_spin() {
+    static const bool v = [] {
+        const char* e = std::getenv("HYOBFS_COALESCE_SPIN");
+        return e && std::atoi(e) != 0;
+    }();
+    return v;
+}
+
 GpuQueue* gpu_queue_new(hyobfs_salamander* c) {
     DeviceGuard g(c->device);
     if (!g.ok) return nullptr;
@@ -581,7 +589,11 @@ GpuQueue* gpu_queue_new(hyobfs_salamander* c) {
     if (!q) return nullptr;
     q->ctx = c;
     bool ok = hipStreamCreateWithFlags(&q->s, hipStreamNonBlocking) == hipSuccess;
-    for (auto& e : q->ev) ok = ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
+    // blocking sync: a coalescer thread waiting for its batch sleeps instead of spinning
+    // (16 connections' threads spinning on one box's CPU share throttled every thread:
+    // millisecond latency tails); HYOBFS_COALESCE_SPIN=1 spins
+    const unsigned fl = hipEventDisableTiming | (coalesce_spin() ? 0u : (unsigned)hipEventBlockingSync);
+    for (auto& e : q->ev) ok = ok && hipEventCreateWithFlags(&e, fl) == hipSuccess;
     if (!ok) {
         gpu_queue_free(q);
         return nullptr;

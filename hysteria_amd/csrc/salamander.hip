@@ -15,7 +15,12 @@
 //     output (configs[2]).  One-shot workgroups per 16 KiB of output.
 //   * salamander_wave_kernel (salamander_wave.h): every other layout (packed
 //     output, ragged lengths, any alignment).  One wave per 64-datagram group.
-#include "salamander_group.h"
+#include <unistd.h>
+
+#include <atomic>
+#include <chrono>
+
+#include "salamander_flat.h"
 
 namespace hyobfs {
 
@@ -32,9 +37,7 @@ namespace hyobfs {
     extern template void launch_flat_sw<true, n>(const BatchParams&, const KeyParams&, const FlatParams&,   \
                                                  hipStream_t);                                              \
     extern template void launch_flat_sw<false, n>(const BatchParams&, const KeyParams&, const FlatParams&,  \
-                                                  hipStream_t);                                             \
-    extern template void launch_group_sw<true, n>(const BatchParams&, const KeyParams&, uint64_t, hipStream_t); \
-    extern template void launch_group_sw<false, n>(const BatchParams&, const KeyParams&, uint64_t, hipStream_t);
+                                                  hipStream_t);
 HY_EXTERN_SW(0) HY_EXTERN_SW(1) HY_EXTERN_SW(2) HY_EXTERN_SW(3) HY_EXTERN_SW(4) HY_EXTERN_SW(5)
 HY_EXTERN_SW(6) HY_EXTERN_SW(7) HY_EXTERN_SW(8) HY_EXTERN_SW(9) HY_EXTERN_SW(10) HY_EXTERN_SW(11)
 HY_EXTERN_SW(12) HY_EXTERN_SW(13) HY_EXTERN_SW(14) HY_EXTERN_SW(15)
@@ -206,9 +209,10 @@ __global__ void synth_bimodal_kernel(uint32_t* dst, uint64_t n, uint64_t seed, u
 // ------------------------------------------------------------------ launchers
 
 // Kernel choice ("Kernels"): AUTO runs the tile kernel where it
-// applies (tile_params), the flat kernel on contiguous input into packed output
-// (flat_eligible) and the wave kernel elsewhere; WAVE forces the wave kernel; TILE
-// and FLAT are AUTO.  HYOBFS_KERNEL=wave|tile|flat sets what AUTO means in a process.
+// applies (tile_params) and the wave kernel elsewhere; WAVE forces the wave kernel;
+// FLAT runs the flat kernel on contiguous input into packed output (flat_eligible)
+// and is AUTO elsewhere; TILE is AUTO.  HYOBFS_KERNEL=wave|tile|flat sets what AUTO
+// means in a process.
 static int kernel_override() {   // HYOBFS_KERNEL, as HYOBFS_KERNEL_* (0 = auto); read once, thread-safe
     static const int v = [] {
         const char* e = std::getenv("HYOBFS_KERNEL");
@@ -253,8 +257,24 @@ static void launch_main(const BatchParams& bp, const KeyParams& k, hipStream_t s
 // (tile_sums_kernel, scan_tiles_kernel).  Otherwise (slotted output, shorter packed
 // runs) a prepass writes the input offsets into the scratch -- length sums, their
 // scan, in_offsets_kernel -- and the kernels for explicit offsets run on them.
-static bool flat_eligible(const BatchParams& b) {   // the flat kernel (salamander_flat.h)
-    return contiguous_input(b) && b.out_stride == 0 && resolve_kernel(b.kernel) != kKernelWave &&
+// A tag no earlier call used (the flat kernel's key records, salamander_flat.h): a
+// process-wide counter from a clock- and pid-derived start, never 0.
+static uint64_t next_epoch() {
+    static std::atomic<uint64_t> ctr{[] {
+        const uint64_t t = (uint64_t)std::chrono::steady_clock::now().time_since_epoch().count();
+        return (t * 0x9e3779b97f4a7c15ull) ^ ((uint64_t)getpid() << 40);
+    }()};
+    uint64_t e;
+    do e = ctr.fetch_add(1, std::memory_order_relaxed) + 1; while (e == 0);
+    return e;
+}
+
+// The flat kernel (salamander_flat.h) runs when asked for (HYOBFS_KERNEL_FLAT, or
+// HYOBFS_KERNEL=flat) on contiguous input into packed output from 16-byte aligned
+// input.  AUTO keeps the wave kernel there: on configs[2] it is faster (1.36-1.42 ms
+// against 1.56-1.68 ms for the flat kernel's best variants, profiles/r06_bimodal/).
+static bool flat_eligible(const BatchParams& b) {
+    return contiguous_input(b) && b.out_stride == 0 && resolve_kernel(b.kernel) == kKernelFlat &&
            (reinterpret_cast<uintptr_t>(b.in) & 15u) == 0;
 }
 static bool wave_scans_input(const BatchParams& b) {   // the wave kernel scans the lengths itself
@@ -269,7 +289,7 @@ uint64_t batch_workspace_bytes(bool obf, const BatchParams& b) {
     if (b.n == 0) return 0;
     const uint64_t tsums = (div_up(b.n, kTile) + 1) * 8;
     if (!contiguous_input(b)) return b.out_stride == 0 ? tsums : 0;
-    if (flat_eligible(b)) return 2 * tsums + flat_workspace_bytes(b.out_cap);
+    if (flat_eligible(b)) return 2 * tsums + flat_workspace_bytes(b.out_cap, b.n);
     return 2 * tsums + (wave_scans_input(b) ? 0 : 8 * b.n);
 }
 
@@ -293,23 +313,6 @@ static hipError_t launch_contiguous(BatchParams& bp, const KeyParams& k, hipStre
     const uint64_t ntiles = div_up(bp.n, kTile);
     bp.tile_sums = static_cast<uint64_t*>(bp.scratch);
     bp.in_tile_sums = bp.tile_sums + ntiles + 1;
-    if (flat_eligible(bp) && resolve_kernel(bp.kernel) != kKernelFlat) {   // sums, their scan, the group kernel
-        const dim3 grid((uint32_t)div_up(ntiles, 4)), block(256);
-        hipLaunchKernelGGL(tile_sums_kernel<OBF>, grid, block, 0, s, bp, ntiles);
-        hipLaunchKernelGGL(scan_tiles_kernel, dim3(2), dim3(1024), 0, s, bp.tile_sums, bp.in_tile_sums, ntiles);
-        bp.tile_prefix = bp.tile_sums;
-        bp.in_tile_prefix = bp.in_tile_sums;
-        switch (k.salt_pos >> 3) {
-#define HY_CASE(n) \
-    case n: launch_group_sw<OBF, n>(bp, k, ntiles, s); break;
-            HY_CASE(0) HY_CASE(1) HY_CASE(2) HY_CASE(3) HY_CASE(4) HY_CASE(5) HY_CASE(6) HY_CASE(7)
-            HY_CASE(8) HY_CASE(9) HY_CASE(10) HY_CASE(11) HY_CASE(12) HY_CASE(13) HY_CASE(14)
-            HY_CASE(15)
-#undef HY_CASE
-        }
-        done = true;
-        return hipGetLastError();
-    }
     if (flat_eligible(bp)) {   // sums, their scan, the locate prepass, the flat kernel
         FlatParams F;
         F.cut = bp.in_tile_sums + ntiles + 1;
@@ -318,6 +321,10 @@ static hipError_t launch_contiguous(BatchParams& bp, const KeyParams& k, hipStre
         F.in_total = bp.in_tile_sums + ntiles;   // the length scan's total
         F.ntiles_max = flat_ntiles_max(bp.out_cap);
         F.t0 = 0;
+        F.krec = reinterpret_cast<uint8_t*>((reinterpret_cast<uintptr_t>(F.cut) + flat_desc_bytes(bp.out_cap) + 255) &
+                                            ~(uintptr_t)255);
+        F.epoch = next_epoch();
+        F.nhash = flat_hashers();
         const dim3 grid((uint32_t)div_up(ntiles, 4)), block(256);
         hipLaunchKernelGGL(tile_sums_kernel<OBF>, grid, block, 0, s, bp, ntiles);
         hipLaunchKernelGGL(scan_tiles_kernel, dim3(2), dim3(1024), 0, s, bp.tile_sums, bp.in_tile_sums, ntiles, F.cut);

@@ -59,12 +59,6 @@ constexpr uint32_t flat_stage_bytes() { return kFT + (OBF ? 32u : 8u * kFD + 32u
 #ifndef HY_FLAT_MIN_WAVES
 #define HY_FLAT_MIN_WAVES 8
 #endif
-#ifndef HY_FLAT_PRIO
-#define HY_FLAT_PRIO 0   // wave priority while hashing (s_setprio), 0 = none
-#endif
-#ifndef HY_FLAT_LAUNCH_TILES
-#define HY_FLAT_LAUNCH_TILES 0   // tiles per launch (0: one launch)
-#endif
 // w[] flag bits above the width (widths are < 2^24)
 constexpr uint32_t kFlatOffWin = 1u << 31;   // some payload byte of the tile lies outside the staged window
 constexpr uint32_t kFlatOffGrid = 1u << 30;  // stage offset not a multiple of 8 from the output offset
@@ -84,12 +78,75 @@ struct FlatParams {
     uint64_t ntiles_max;
     const uint64_t* in_total;    // input bytes: the length scan's total (device)
     const uint64_t* out_total;   // the width scan's total: the valid output's end without a cut
-    uint64_t t0;        // first tile of this launch
+    uint64_t t0;        // unused (one launch)
+    uint8_t* krec;      // key records: per datagram 4 granules {key word, epoch} (krec_*)
+    uint64_t epoch;     // this call's tag (never 0)
+    uint32_t nhash;     // hasher workgroups in front of the tile workgroups
 };
 
 inline uint64_t flat_ntiles_max(uint64_t out_cap) { return (out_cap + kFT - 1) / kFT; }
-// the prepass's scratch: two header words, the descriptor of every tile out_cap allows
-inline uint64_t flat_workspace_bytes(uint64_t out_cap) { return 16 + sizeof(FlatDesc) * (flat_ntiles_max(out_cap) + 1); }
+constexpr uint64_t kKeyRec = 64;   // key record bytes per datagram
+// the prepass's scratch: two header words, the descriptor of every tile out_cap allows,
+// then (256-aligned) the key records
+inline uint64_t flat_desc_bytes(uint64_t out_cap) { return 16 + sizeof(FlatDesc) * (flat_ntiles_max(out_cap) + 1); }
+inline uint64_t flat_workspace_bytes(uint64_t out_cap, uint64_t n) {
+    return ((flat_desc_bytes(out_cap) + 255) & ~255ull) + 256 + kKeyRec * n;
+}
+
+// Hasher workgroups per launch (HYOBFS_FLAT_HASHERS overrides; 0: every tile hashes its
+// own keys).  64 x 4 waves hash configs[2]'s 4M keys in ~0.9 ms, ahead of the tiles.
+#ifndef HY_FLAT_HASHERS
+#define HY_FLAT_HASHERS 256
+#endif
+#ifndef HY_FLAT_HASH_PRIO
+#define HY_FLAT_HASH_PRIO 3
+#endif
+inline uint32_t flat_hashers() {
+    static const uint32_t v = [] {
+        const char* e = std::getenv("HYOBFS_FLAT_HASHERS");
+        const long x = e ? std::atol(e) : HY_FLAT_HASHERS;
+        return (uint32_t)(x < 0 ? 0 : x > 4096 ? 4096 : x);
+    }();
+    return v;
+}
+
+// ---- key records: the hand-off from the hasher workgroups to the tile workgroups
+// inside one launch (MI355X_MICROARCH.md, inter-workgroup visibility; the per-XCD L2s
+// are not coherent).  Datagram k's record is four 16-byte granules {key word w,
+// epoch}, each written by ONE write-through (sc1) 16-byte store and read by ONE sc1
+// 16-byte load: a granule carries its own tag, so a reader never needs a flag or a
+// fence -- a tag equal to this call's epoch means that word is this call's key
+// (records of earlier calls carry other epochs).
+#ifdef HYOBFS_EMULATE
+__device__ __forceinline__ void krec_store(uint8_t* blk, uint32_t off, uint64_t w, uint64_t tag) {
+    std::memcpy(blk + off, &w, 8);
+    std::memcpy(blk + off + 8, &tag, 8);
+}
+__device__ __forceinline__ void krec_load(const uint8_t* blk, uint32_t off, uint64_t& w, uint64_t& tag) {
+    std::memcpy(&w, blk + off, 8);
+    std::memcpy(&tag, blk + off + 8, 8);
+}
+#else
+typedef uint32_t krec_v4 __attribute__((ext_vector_type(4)));
+// blk: wave-uniform base of a 64-record (4 KiB) block
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t krec_rsrc(const uint8_t* blk) {
+    const uint64_t a = uni64(reinterpret_cast<uint64_t>(blk));
+    return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(a), 0, (int)(64 * kKeyRec), 0x00020000);
+}
+__device__ __forceinline__ void krec_store(uint8_t* blk, uint32_t off, uint64_t w, uint64_t tag) {
+    krec_v4 v;
+    v.x = (uint32_t)w;
+    v.y = (uint32_t)(w >> 32);
+    v.z = (uint32_t)tag;
+    v.w = (uint32_t)(tag >> 32);
+    __builtin_amdgcn_raw_buffer_store_b128(v, krec_rsrc(blk), (int)off, 0, 16);   // aux 16: sc1
+}
+__device__ __forceinline__ void krec_load(const uint8_t* blk, uint32_t off, uint64_t& w, uint64_t& tag) {
+    const krec_v4 v = __builtin_amdgcn_raw_buffer_load_b128(krec_rsrc(blk), (int)off, 0, 16);   // sc1
+    w = (uint64_t)v.y << 32 | v.x;
+    tag = (uint64_t)v.w << 32 | v.z;
+}
+#endif
 
 // Per datagram: width (drop rules), output and input offsets from the scans, the
 // reference's return values, and the descriptor of every tile whose first byte the
@@ -286,6 +343,47 @@ __device__ __forceinline__ bool flat_chunk(const LDS& S, int32_t rel, uint32_t k
     return true;
 }
 
+// A hasher workgroup: its waves take 64-datagram blocks in index order (block
+// h * waves + wave, then every nhash * waves), one lane per key (wave_key,
+// salamander_wave.h: the fewest instructions per key), and publish each key as a
+// record of four tagged granules.  Deobfuscate reads the wire salts at the offsets
+// from the length scan.  Hashers never wait on anything.
+template <bool OBF, int SW>
+__device__ __forceinline__ void flat_hasher(const BatchParams& B, const KeyParams& K, const FlatParams& F, uint32_t h,
+                                            uint32_t wid) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t step = (uint64_t)F.nhash * kFWaves;
+#ifndef HYOBFS_EMULATE
+    __builtin_amdgcn_s_setprio(HY_FLAT_HASH_PRIO);   // VALU-only waves among streaming ones: issue first
+#endif
+    for (uint64_t blk = (uint64_t)h * kFWaves + wid; blk * 64 < B.n; blk += step) {
+        const uint64_t k = blk * 64 + lane;
+        const bool live = k < B.n;
+        uint64_t salt = 0;
+        if (OBF) {
+            salt = live ? B.salts[k] : 0ull;
+        } else {   // the wire's salt at the datagram's input offset
+            const uint64_t g = blk / 4;   // its 256-datagram scan tile
+            uint64_t pre = 0;
+#pragma unroll
+            for (int j = 0; j < 3; ++j) {
+                const uint64_t q = g * kTile + 64ull * j + lane;
+                if (q < blk * 64) pre += B.in_len[q];
+            }
+            const uint32_t L = live ? B.in_len[k] : 0u;
+            const uint64_t i = B.in_tile_prefix[g] + wave_sum(pre) + wave_incl_scan32(L, (int)lane) - L;
+            if (L > 8u) salt = load8u(B.in + i);
+        }
+        uint64_t key[4];
+        wave_key<SW>(K, salt, key);
+        uint8_t* kb = F.krec + kKeyRec * blk * 64;
+        if (live) {
+#pragma unroll
+            for (int w = 0; w < 4; ++w) krec_store(kb, (uint32_t)(kKeyRec * lane + 16 * w), key[w], F.epoch);
+        }
+    }
+}
+
 template <bool OBF, int SW>
 __global__ __launch_bounds__(kFThreads, HY_FLAT_MIN_WAVES) void salamander_flat_kernel(BatchParams B, KeyParams K,
                                                                                   FlatParams F) {
@@ -294,7 +392,11 @@ __global__ __launch_bounds__(kFThreads, HY_FLAT_MIN_WAVES) void salamander_flat_
     __shared__ __attribute__((aligned(16))) FlatLDS<OBF> S;
     const uint32_t wid = uni32(threadIdx.x >> 6);
     const uint8_t* __restrict__ in = B.in;
-    const uint64_t t = F.t0 + blockIdx.x;
+    if (blockIdx.x < F.nhash) {   // a hasher workgroup (whole workgroup)
+        flat_hasher<OBF, SW>(B, K, F, blockIdx.x, wid);
+        return;
+    }
+    const uint64_t t = blockIdx.x - F.nhash;
     const uint64_t E = uni64(min<uint64_t>(F.cut[0], *F.out_total));   // end of the valid output
     if (t == 0 && threadIdx.x == 0 && B.out_total) atomicAdd(B.out_total, (unsigned long long)E);
     const uint64_t tT = t * kFT;
@@ -334,42 +436,63 @@ __global__ __launch_bounds__(kFThreads, HY_FLAT_MIN_WAVES) void salamander_flat_
         asm volatile("" : "+v"(tid));
 #endif
         const uint32_t lane = tid & 63;
-        // ---- 2. every wave: the pass's lengths, widths, offsets and salts (lane l: datagram g0 + l)
-        const bool live = lane < m;
-        const uint64_t p = g0 + lane;
-        const uint32_t L = live ? B.in_len[p] : 0u;
-        uint64_t salt = live && OBF ? B.salts[p] : 0ull;
-        uint32_t W = live ? out_width<OBF>(L, B.pkt_cap) : 0u;
-        // tile-relative 32-bit scans: a pass spans at most 64 x 2^24 bytes
-        const uint32_t iw = wave_incl_scan32(W, (int)lane);
-        const uint32_t il = wave_incl_scan32(L, (int)lane);
-        const uint64_t o = og + iw - W, i = ig + il - L;
-        og += uni32((uint32_t)__shfl(iw, 63, 64));
-        ig += uni32((uint32_t)__shfl(il, 63, 64));
-        if (W && o + W > B.out_cap) W = 0;   // past out_cap: dropped (not in [d0, dend) unless cut)
-        if (!OBF && W) salt = load8u(in + i);   // the wire's salt
-        const int32_t orel = (int32_t)((int64_t)o - (int64_t)tT);
-        const int32_t dlt = (int32_t)((int64_t)(i + SKIP) - (int64_t)ws) - (orel + SALT);
-        // ---- keys: wave w hashes datagrams 16w .. 16w + 15, four lanes each, rotated
-        // to the output's 32-byte phase (byte x of the row: key byte x - (o + SALT) mod 32)
-        if (16u * wid < m) {
-            const uint32_t k = 16u * wid + (lane >> 2), qi = lane & 3u;
-            const uint64_t sk = __shfl(salt, (int)k, 64);
-            const uint32_t ok = (uint32_t)__shfl((uint32_t)o, (int)k, 64);
-#if HY_FLAT_PRIO && !defined(HYOBFS_EMULATE)
-            __builtin_amdgcn_s_setprio(HY_FLAT_PRIO);   // the hash is the tile's latency chain
-#endif
-            const uint64_t kw = quad_key<SW>(K, sk, qi);
-#if HY_FLAT_PRIO && !defined(HYOBFS_EMULATE)
-            __builtin_amdgcn_s_setprio(0);
-#endif
-            const uint32_t rr = (ok + (uint32_t)SALT) & 31u;
-            const uint32_t st = (8u * qi - rr) & 31u, w0 = st >> 3, sh = (st & 7u) * 8u;
-            const uint64_t a = __shfl(kw, (int)((lane & ~3u) | w0), 64);
-            const uint64_t b = __shfl(kw, (int)((lane & ~3u) | ((w0 + 1) & 3u)), 64);
-            if (k < m) S.key[k][qi] = sh ? (a >> sh) | (b << (64 - sh)) : a;
-        }
         if (wid == 0) {
+            // ---- 2. wave 0: the pass's lengths, widths, offsets, salts and key records
+            // (lane l: datagram g0 + l), all loaded in one round trip
+            const bool live = lane < m;
+            const uint64_t p = g0 + lane;
+            const uint32_t L = live ? B.in_len[p] : 0u;
+            uint64_t salt = live && OBF ? B.salts[p] : 0ull;
+            uint8_t* kb = F.krec + kKeyRec * g0;   // the pass's first record (64 records: one 4 KiB block)
+            uint64_t kw[4], tg[4];
+#pragma unroll
+            for (int w = 0; w < 4; ++w) {
+                kw[w] = tg[w] = 0;
+                if (live) krec_load(kb, (uint32_t)(kKeyRec * lane + 16 * w), kw[w], tg[w]);
+            }
+            uint32_t W = live ? out_width<OBF>(L, B.pkt_cap) : 0u;
+            // tile-relative 32-bit scans: a pass spans at most 64 x 2^24 bytes
+            const uint32_t iw = wave_incl_scan32(W, (int)lane);
+            const uint32_t il = wave_incl_scan32(L, (int)lane);
+            const uint64_t o = og + iw - W, i = ig + il - L;
+            og += uni32((uint32_t)__shfl(iw, 63, 64));
+            ig += uni32((uint32_t)__shfl(il, 63, 64));
+            if (W && o + W > B.out_cap) W = 0;   // past out_cap: dropped (not in [d0, dend) unless cut)
+            const int32_t orel = (int32_t)((int64_t)o - (int64_t)tT);
+            const int32_t dlt = (int32_t)((int64_t)(i + SKIP) - (int64_t)ws) - (orel + SALT);
+            // ---- keys: the hashers' records; a record not published yet is polled a
+            // while, then the wave hashes the pass's keys itself (four lanes per key)
+            bool miss = W && (tg[0] != F.epoch || tg[1] != F.epoch || tg[2] != F.epoch || tg[3] != F.epoch);
+            for (int spin = 0; spin < 48 && __ballot(miss); ++spin) {
+#ifndef HYOBFS_EMULATE
+                __builtin_amdgcn_s_sleep(8);
+#endif
+                if (miss) {
+                    miss = false;
+#pragma unroll
+                    for (int w = 0; w < 4; ++w) {
+                        krec_load(kb, (uint32_t)(kKeyRec * lane + 16 * w), kw[w], tg[w]);
+                        miss |= tg[w] != F.epoch;
+                    }
+                }
+            }
+            if (__ballot(miss)) {   // fallback: quad hashes, 16 keys per pass of the wave
+                if (!OBF && W) salt = load8u(in + i);   // the wire's salt
+                for (uint32_t k0 = 0; k0 < m; k0 += 16) {
+                    const uint32_t k = k0 + (lane >> 2), qi = lane & 3u;
+                    const uint64_t x = quad_key<SW>(K, __shfl(salt, (int)(k < 64 ? k : 0), 64), qi);
+                    // lane l collects words 0..3 of key l from lanes 4(l - k0) + w
+                    const uint32_t src = 4u * ((lane - k0) & 15u);
+#pragma unroll
+                    for (int w = 0; w < 4; ++w) {
+                        const uint64_t y = __shfl(x, (int)(src + (uint32_t)w), 64);
+                        if (miss && lane >= k0 && lane < k0 + 16) kw[w] = y;
+                    }
+                }
+            }
+            // rotated to the output's 32-byte phase: row byte x = key byte x - (o + SALT) mod 32
+            uint64_t kr[4];
+            rotl_key_bytes(kw, ((uint32_t)o + (uint32_t)SALT) & 31u, kr);
             // the tile's part of the payload inside the staged window, on the 8-byte grid
             uint32_t fl = 0;
             if (W) {
@@ -382,6 +505,8 @@ __global__ __launch_bounds__(kFThreads, HY_FLAT_MIN_WAVES) void salamander_flat_
             S.w[lane] = W | fl;
             S.dlt[lane] = dlt;
             S.salt[lane] = salt;
+#pragma unroll
+            for (int w = 0; w < 4; ++w) S.key[lane][w] = kr[w];
         }
         __syncthreads();   // the stage has landed (every wave's vmcnt(0)), the table and keys are published
 
@@ -427,16 +552,11 @@ __global__ __launch_bounds__(kFThreads, HY_FLAT_MIN_WAVES) void salamander_flat_
 
 template <bool OBF, int SW>
 void launch_flat_sw(const BatchParams& b, const KeyParams& k, const FlatParams& F, hipStream_t s) {
-    // one workgroup per tile out_cap allows (those past the valid output exit at once);
-    // at least one, which writes out_total
+    // the hashers, then one workgroup per tile out_cap allows (those past the valid
+    // output exit at once; at least one, which writes out_total)
     const uint64_t nt = F.ntiles_max < 1 ? 1 : F.ntiles_max;
-    const uint64_t per = HY_FLAT_LAUNCH_TILES ? (uint64_t)HY_FLAT_LAUNCH_TILES : nt;
-    for (uint64_t t0 = 0; t0 < nt; t0 += per) {
-        FlatParams Fl = F;
-        Fl.t0 = t0;
-        const uint64_t g = nt - t0 < per ? nt - t0 : per;
-        hipLaunchKernelGGL((salamander_flat_kernel<OBF, SW>), dim3((uint32_t)g), dim3(kFThreads), 0, s, b, k, Fl);
-    }
+    hipLaunchKernelGGL((salamander_flat_kernel<OBF, SW>), dim3((uint32_t)(F.nhash + nt)), dim3(kFThreads), 0, s, b, k,
+                       F);
 }
 
 }  // namespace hyobfs

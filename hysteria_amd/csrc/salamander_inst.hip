@@ -1,6 +1,6 @@
 // salamander_inst.hip -- instantiates the batch kernels for one salt word
 // (compiled once per HY_SW = 0..15, see Makefile).
-#include "salamander_group.h"
+#include "salamander_flat.h"
 
 #ifndef HY_SW
 #error "compile with -DHY_SW=<salt word 0..15>"
@@ -15,6 +15,4 @@ template void launch_tile_sw<true, HY_SW>(const BatchParams&, const KeyParams&, 
 template void launch_tile_sw<false, HY_SW>(const BatchParams&, const KeyParams&, const TileParams&, hipStream_t);
 template void launch_flat_sw<true, HY_SW>(const BatchParams&, const KeyParams&, const FlatParams&, hipStream_t);
 template void launch_flat_sw<false, HY_SW>(const BatchParams&, const KeyParams&, const FlatParams&, hipStream_t);
-template void launch_group_sw<true, HY_SW>(const BatchParams&, const KeyParams&, uint64_t, hipStream_t);
-template void launch_group_sw<false, HY_SW>(const BatchParams&, const KeyParams&, uint64_t, hipStream_t);
 }  // namespace hyobfs

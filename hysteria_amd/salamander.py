@@ -139,9 +139,10 @@ class SalamanderObfuscator:
     KERNELS = {"auto": 0, "wave": 1, "tile": 2, "flat": 3}
 
     def set_kernel(self, kernel: str) -> None:
-        """Batch kernel of this context: "auto" (the tile kernel where it applies, the flat
-        kernel on contiguous input into packed output, else the wave-group kernel), "wave"
-        (forced), "tile" or "flat" (= auto; include/hyobfs.h, HYOBFS_KERNEL_*)."""
+        """Batch kernel of this context: "auto" (the tile kernel where it applies, else the
+        wave-group kernel), "wave" (forced), "flat" (the flat kernel on contiguous input
+        into packed output, auto elsewhere) or "tile" (= auto; include/hyobfs.h,
+        HYOBFS_KERNEL_*)."""
         check(self._lib.hyobfs_salamander_set_kernel(self._h, self.KERNELS[kernel]), "set_kernel")
         self.kernel = kernel
 

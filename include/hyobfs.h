@@ -57,11 +57,12 @@ extern "C" {
 #endif
 
 /* ABI version.  4 (this header) against 3:
- *   - new kernel HYOBFS_KERNEL_FLAT (3): contiguous input into packed output runs
- *     the flat kernel under AUTO (16-byte aligned in and out); 3 meant STREAM in
- *     ABI 2 and was rejected in ABI 3;
- *   - contiguous input with packed output needs more scratch (the flat prepass's
- *     tile descriptors, 24 B per 16 KiB of out_cap): ask hyobfs_batch_workspace_bytes;
+ *   - new kernel HYOBFS_KERNEL_FLAT (3): contiguous input into packed output on the
+ *     flat kernel (16-byte aligned in; 3 meant STREAM in ABI 2 and was rejected in
+ *     ABI 3);
+ *   - contiguous input with packed output needs more scratch (the flat kernel's tile
+ *     descriptors, 24 B per 16 KiB of out_cap, and key records, 64 B per datagram):
+ *     ask hyobfs_batch_workspace_bytes;
  *   - hyobfs_conn_free on a connection that was never closed closes its fd (in ABI 2
  *     it detached and left the socket open; include/hyobfs_conn.h).
  * 3 against 2:
@@ -134,12 +135,14 @@ int hyobfs_salamander_device(const hyobfs_salamander* ctx);
    HYOBFS_KERNEL_AUTO runs the tile kernel on slotted batches whose region edges
    are all multiples of 8 (one length, slot and input stride multiples of 8,
    payloads of 16 bytes or more, nothing dropped) -- the uniform 1200-byte batch
-   of the benchmark --, the flat kernel on contiguous input into packed output
-   (16-byte aligned in; the ragged configs[2] batch), and the wave-group kernel on
-   every other batch (packed output, ragged lengths, any alignment).
-   HYOBFS_KERNEL_WAVE forces the wave-group kernel; HYOBFS_KERNEL_TILE and
-   HYOBFS_KERNEL_FLAT are AUTO.  The HYOBFS_KERNEL environment variable
-   (wave|tile|flat) overrides AUTO.  Returns HYOBFS_ERR_INVALID for an unknown value.
+   of the benchmark -- and the wave-group kernel on every other batch (packed
+   output, ragged lengths, any alignment; contiguous input scans its lengths
+   alongside the widths).  HYOBFS_KERNEL_WAVE forces the wave-group kernel;
+   HYOBFS_KERNEL_FLAT runs the flat kernel on contiguous input into packed output
+   from 16-byte aligned input (one-shot workgroups per 16 KiB of output, keys from
+   hasher workgroups; measured slower than the wave kernel on the ragged configs[2]
+   batch) and is AUTO elsewhere; HYOBFS_KERNEL_TILE is AUTO.  The
+   HYOBFS_KERNEL environment variable (wave|tile|flat) overrides AUTO.  Returns HYOBFS_ERR_INVALID for an unknown value.
    May be called while other threads run batches on the context (an atomic
    setting; a batch uses the value it read when it started).  Outputs are
    identical. */
@@ -236,8 +239,9 @@ typedef struct hyobfs_batch {
 uint64_t hyobfs_batch_workspace_size(uint64_t n);
 /* Scratch any batch needs, whatever the kernel choice: the above for packed
    batches with explicit offsets; for contiguous input twice that (width and
-   length sums), plus, into packed output, 16 B + 24 B per 16 KiB of out_cap (the
-   flat kernel's tile descriptors), or, into slotted output (or with
+   length sums), plus, into packed output from 16-byte aligned input, the flat
+   kernel's scratch (16 B + 24 B per 16 KiB of out_cap, rounded up to 256, + 256 B
+   + 64 B per datagram), or, into slotted output (or with
    HYOBFS_PACKED_RUN_LOG2 shortening the packed runs), 8 B per datagram (the input
    offsets a prepass writes); 0 for other slotted batches. */
 uint64_t hyobfs_batch_workspace_bytes(const hyobfs_batch* b);

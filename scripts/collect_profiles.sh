@@ -11,7 +11,7 @@ TAG=${1:-r02}
 cd /tmp && export TMPDIR=/tmp
 cp "$R/profiles/pmc_traffic.json" "$O/pmc_traffic.json" 2>/dev/null || echo '{"entries": []}' > "$O/pmc_traffic.json"
 # 1. HBM traffic: FETCH_SIZE and WRITE_SIZE in separate passes, per workload
-for wl in uniform bimodal; do
+for wl in uniform bimodal uniform8m; do   # uniform8m: the N > 1 shard (bench.py at --gpus > 1)
   for c in FETCH_SIZE WRITE_SIZE; do
     timeout -k 10 240 rocprofv3 --pmc $c --kernel-trace --output-format csv -d "$O/$wl/pmc_$c" -o run -- \
       python3 "$R/scripts/prof_one.py" $wl 5 > "$O/$wl.pmc_$c.log" 2>&1 || { echo "pmc $wl $c failed"; exit 1; }

@@ -20,7 +20,8 @@
 #                   of scripts/prof_one.py WL K (PT=1: output buffers pre-touched); scripts/clock_trace.py
 #   clkbench:W      the same counters over the bench command (bench.py --steps 20 --warmup W)
 #   kt:WL:K         rocprofv3 --kernel-trace --stats of scripts/prof_one.py WL K (per-kernel times)
-#   udp:M:P:T:W     tools/udp_bench M P 4 1200 1024 T W (loopback PacketConn rate; M = batch|raw|coalesce|single)
+#   udp:M:P:T:W[:R] tools/udp_bench M P 4 1200 1024 T W R (loopback PacketConn rate; M = batch|raw|coalesce|single;
+#                   R = offered datagrams/s, 0 or absent = saturated)
 #   bsq:KERN:SUF    SQ/TCC counter groups of the configs[2] batch under kernel KERN (pmc_bimodal_sq.sh)
 #   ab              in-process A/B of library builds (scripts/ab_variants.py; AB_* env vars)
 #   abg             the same for Gecko builds (scripts/ab_gecko_variants.py)
@@ -77,8 +78,9 @@ for s in "$@"; do
     kt:*) IFS=: read -r _ WL K <<< "$s"
             (cd /tmp && export TMPDIR=/tmp && step "kt $WL $K" 240 rocprofv3 --kernel-trace --stats --output-format csv \
               -d "$O/kt_${WL}_$K" -o run -- python3 "$R/scripts/prof_one.py" "$WL" "$K" > "$O/kt_${WL}_$K.log" 2>&1) || exit 1 ;;
-    udp:*) IFS=: read -r _ M P T W <<< "$s"
-            step "udp $M $P $T $W" 120 tools/udp_bench "$M" "$P" 4 1200 1024 "$T" "$W" > "$O/udp_${M}_${P}x${T}_w$W.json" ;;
+    udp:*) IFS=: read -r _ M P T W RATE <<< "$s"
+            step "udp $M $P $T $W ${RATE:-0}" 120 tools/udp_bench "$M" "$P" 4 1200 1024 "$T" "$W" "${RATE:-0}" \
+              > "$O/udp_${M}_${P}x${T}_w${W}_r${RATE:-0}.json" ;;
     bsq:*) IFS=: read -r _ KERN SUF <<< "$s"   # SQ/TCC counter groups of the configs[2] batch (scripts/pmc_bimodal_sq.sh)
             step "bsq $KERN" 700 bash scripts/pmc_bimodal_sq.sh "$KERN" "$SUF" > "$O/bsq_$KERN$SUF.log" 2>&1 ;;
     ab) step ab 600 python -u scripts/ab_variants.py ${AB_ARGS:-} > "$O/ab_${AB_NAME:-run}.txt" 2>&1 ;;

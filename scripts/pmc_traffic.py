@@ -14,8 +14,8 @@ from bench import kernel_src_sha  # noqa: E402
 
 root, wl, src, dst = sys.argv[1:5]
 label = sys.argv[5] if len(sys.argv) > 5 else root
-MAIN = {True: re.compile(r"salamander_(tile_kernel|wave_kernel)<true"),
-        False: re.compile(r"salamander_(tile_kernel|wave_kernel)<false")}
+MAIN = {True: re.compile(r"salamander_(tile_kernel|wave_kernel|flat_kernel)<true"),
+        False: re.compile(r"salamander_(tile_kernel|wave_kernel|flat_kernel)<false")}
 
 
 def per_batch(counter, obf):
@@ -41,9 +41,10 @@ def per_batch(counter, obf):
 
 
 BATCHES = int(os.environ.get("PMC_BATCHES", "5"))
-if wl == "uniform":
-    P, L = 1 << 20, 1200
+if wl in ("uniform", "uniform8m"):   # uniform8m: configs[3]'s 8M shard, stored as workload "uniform"
+    P, L = (1 << 20) if wl == "uniform" else (1 << 23), 1200
     alg = {True: P * (2 * L + 16), False: P * (2 * L + 8)}
+    wl = "uniform"
 else:
     from oracle.salamander_ref import COracle
     P, L = 1 << 22, "bimodal"
@@ -63,7 +64,7 @@ for obf in (True, False):
         continue
     fetch, write = 2 * fetch_kib * 1024, write_kib * 1024
     entries = [e for e in entries if not (e.get("src_sha") == sha and e.get("workload") == wl
-                                          and e.get("direction") == direction)]
+                                          and e.get("direction") == direction and e.get("datagrams") == P)]
     entries.append({
         "src_sha": sha, "workload": wl, "direction": direction, "datagrams": P, "len": L,
         "kernel": " | ".join(sorted(n1 | n2)), "fetch_size_kib_raw": fetch_kib, "write_size_kib": write_kib,

@@ -1,6 +1,7 @@
 """Minimal driver for rocprofv3 counter passes: K obfuscate + K deobfuscate launches
 of the uniform 1M x 1200 B batch (BASELINE configs[1]), or of the 4M bimodal
-batch (configs[2], packed output) with 'bimodal' (contiguous input, as bench.py) or
+batch (configs[2], packed output) with 'bimodal'; 'uniform8m': the 8M x 1200 B shard of
+configs[3] (one rank at N > 1) (contiguous input, as bench.py) or
 'bimodal_off' (explicit offsets); 'bimodal_alt': 20 warm-up obfuscate launches, then
 K of each layout alternating (obfuscate only).  Optional 3rd argument: the context's
 kernel (auto|wave|tile).  PROF_PRETOUCH=1 writes zeros over every output buffer (and
@@ -13,8 +14,8 @@ import torch, hysteria_amd
 wl = sys.argv[1] if len(sys.argv) > 1 else "uniform"
 K = int(sys.argv[2]) if len(sys.argv) > 2 else 5
 kern = sys.argv[3] if len(sys.argv) > 3 else "auto"
-if wl not in ("uniform", "uniform_rev", "bimodal", "bimodal_off", "bimodal_alt"):
-    sys.exit(f"unknown workload {wl!r}: uniform | uniform_rev | bimodal | bimodal_off | bimodal_alt")
+if wl not in ("uniform", "uniform8m", "uniform_rev", "bimodal", "bimodal_off", "bimodal_alt"):
+    sys.exit(f"unknown workload {wl!r}: uniform | uniform8m | uniform_rev | bimodal | bimodal_off | bimodal_alt")
 dev = torch.device("cuda:0")
 o = hysteria_amd.SalamanderObfuscator(b"average_password", 0)
 o.set_kernel(kern)
@@ -28,8 +29,8 @@ if wl == "uniform_rev":
         o.deobfuscate_batch(wire, P, in_stride=L + 8, len_uniform=L + 8, out=back, out_stride=L)
     for _ in range(K):
         o.obfuscate_batch(inp, P, in_stride=L, len_uniform=L, salts=salts, out=wire, out_stride=L + 8)
-elif wl == "uniform":
-    P, L = 1 << 20, 1200
+elif wl in ("uniform", "uniform8m"):   # uniform8m: the 8M-datagram shard a rank runs at N > 1
+    P, L = (1 << 20) if wl == "uniform" else (1 << 23), 1200
     inp = torch.empty(P * L, dtype=torch.uint8, device=dev); hysteria_amd.synth_stream(inp, P * L, 1, 0)
     salts = torch.empty(P, dtype=torch.int64, device=dev); hysteria_amd.synth_u64(salts, P, 2, 0)
     wire = torch.empty(P * (L + 8), dtype=torch.uint8, device=dev); back = torch.empty(P * L, dtype=torch.uint8, device=dev)

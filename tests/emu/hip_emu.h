@@ -230,7 +230,7 @@ inline hipError_t hipOccupancyMaxActiveBlocksPerMultiprocessor(int* nb, K, int, 
 }
 inline hipError_t hipStreamCreateWithFlags(hipStream_t* s, unsigned) { *s = (hipStream_t)1; return hipSuccess; }
 inline hipError_t hipStreamDestroy(hipStream_t) { return hipSuccess; }
-enum { hipEventDisableTiming = 2 };
+enum { hipEventDisableTiming = 2, hipEventBlockingSync = 1 };
 // Events are numbered in creation order (1, 2, ...).  Fault injection for the CPU tier:
 // HYEMU_FAIL_EVENTS_FROM=k makes hipEventSynchronize fail for every event numbered k or
 // later (a coalescing connection's send queue creates events 1-4 and its receive queue

@@ -97,9 +97,9 @@ def case_packed_cap(seed, n, maxlen, obf, cap_pct, psk_len):
 
 def case_contig(seed, n, dist, obf, cap_pct, psk_len, pkt_cap=0, misalign=0, out_stride=0):
     """Contiguous input (in_off NULL, in_stride 0: datagram i right after datagram
-    i-1) into packed output (out_stride 0: the flat kernel under AUTO from 16-byte
-    aligned input; the wave kernel, forced or for misaligned input, scans the lengths
-    itself, and with HYOBFS_PACKED_RUN_LOG2 < 6 a prepass writes the input offsets)
+    i-1) into packed output (out_stride 0: the wave kernel scans the lengths itself,
+    with HYOBFS_PACKED_RUN_LOG2 < 6 a prepass writes the input offsets; with
+    HYOBFS_KERNEL=flat and 16-byte aligned input the flat kernel)
     or into slots of out_stride bytes (the prepass's offsets, then the wave kernel).  dist 0: the
     bimodal 64/1350 mix; 1: 0..2100 B; 2: 0..40 B (several datagrams per chunk);
     3: 1000..5000 B; 4: bimodal with zero-length ones.  out_cap cut to cap_pct % of
@@ -143,13 +143,14 @@ def case_contig(seed, n, dist, obf, cap_pct, psk_len, pkt_cap=0, misalign=0, out
     full = n * out_stride if out_stride else total + (8 * n if obf else 0)
     cap = max(16, full * cap_pct // 100)
     tsums = ((n + 255) // 256 + 1) * 8
-    # packed output from 16-byte aligned input: the flat kernel under AUTO
-    flat = not out_stride and not misalign and os.environ.get("HYOBFS_KERNEL") != "wave"
+    # packed output from 16-byte aligned input: the flat kernel when asked for (HYOBFS_KERNEL=flat)
+    flat = not out_stride and not misalign and os.environ.get("HYOBFS_KERNEL") == "flat"
     prepass = out_stride or os.environ.get("HYOBFS_PACKED_RUN_LOG2", "6") != "6"
     # hyobfs_batch_workspace_bytes: the largest need over the kernel choices
     ws = 2 * tsums + (8 * n if prepass else 0)   # the wave kernel's
     if not out_stride and not misalign:           # the flat kernel's tile descriptors (16 KiB tiles)
-        ws = max(ws, 2 * tsums + 16 + 24 * ((cap + 16383) // 16384 + 1))
+        desc = 16 + 24 * ((cap + 16383) // 16384 + 1)   # + the hashers' key records, 64 B per datagram
+        ws = max(ws, 2 * tsums + ((desc + 255) // 256) * 256 + 256 + 64 * n)
     run(obf, psk, lens, in_off, inp, salts, cap, pkt_cap=pkt_cap, contiguous=True,
         out_stride=out_stride, expect_kernel="flat" if flat else "wave", expect_ws=ws)
 

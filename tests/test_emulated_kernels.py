@@ -49,9 +49,10 @@ SPECS = {
     "test_emulated_contiguous_input_slotted": lambda p: ("contig", p["args"], {"HYEMU_CUS": "2"}),
     "test_emulated_rx_gpu_failure_reports_eio": lambda p: ("rxfail", "", {"HYEMU_FAIL_EVENTS_FROM": "5"}),
     "test_emulated_contiguous_input_auto": lambda p: ("contig", p["args"], {"HYEMU_CUS": "2"}),
-    "test_emulated_contiguous_input_wave": lambda p: ("contig", p["args"], {"HYEMU_CUS": "2", "HYOBFS_KERNEL": "wave"}),
+    "test_emulated_contiguous_input_flat": lambda p: ("contig", p["args"], {"HYEMU_CUS": "2", "HYOBFS_KERNEL": "flat",
+                                                                           "HYOBFS_FLAT_HASHERS": p["hashers"]}),
     "test_emulated_contiguous_input_prepass_offsets": lambda p: ("contig", p["args"], {
-        "HYEMU_CUS": "2", "HYOBFS_PACKED_RUN_LOG2": "3", "HYOBFS_KERNEL": "wave"}),
+        "HYEMU_CUS": "2", "HYOBFS_PACKED_RUN_LOG2": "3"}),
 }
 
 
@@ -154,15 +155,16 @@ PACKED_CASES = [
 
 # Contiguous input (in_off NULL, in_stride 0; tests/emu/run_case.py case_contig:
 # seed n dist obf cap% psk_len [pkt_cap misalign out_stride]).  Packed output under
-# AUTO: the flat kernel (16 KiB output tiles, salamander_flat.h) from 16-byte aligned
-# input, the wave kernel from misaligned input; forced to the wave kernel: the wave
-# kernel taking its input offsets from the scan of the lengths, or, with packed runs
-# of 8, the prepass's input offsets (in_offsets_kernel).  Bimodal, 0..2100 B, tiny
-# (several datagrams per chunk, tiles of several passes), 1-5 KB, zero-length
-# datagrams; out_cap cuts, pkt_cap drops (dropped input inside a tile's window), real
-# wire with 8-byte datagrams, PSKs across salt words and the two-block case, a
-# misaligned input.  The flat kernel's emulation costs a 256-thread workgroup per
-# 16 KiB of output, so its cases are a few hundred KB.
+# AUTO: the wave kernel taking its input offsets from the scan of the lengths, or,
+# with packed runs of 8, the prepass's input offsets (in_offsets_kernel); under
+# HYOBFS_KERNEL=flat from 16-byte aligned input the flat kernel (16 KiB output tiles,
+# salamander_flat.h), its keys from the hasher workgroups (4 hashers: published key
+# records) or, with none, hashed by each tile after its poll gives up (the fallback).
+# Bimodal, 0..2100 B, tiny (several datagrams per chunk, tiles of several passes),
+# 1-5 KB, zero-length datagrams; out_cap cuts, pkt_cap drops (dropped input inside a
+# tile's window), real wire with 8-byte datagrams, PSKs across salt words and the
+# two-block case, a misaligned input (the wave kernel).  The flat kernel's emulation
+# costs a 256-thread workgroup per 16 KiB of output, so its cases are a few hundred KB.
 CONTIG_CASES = [
     "1 3000 0 1 100 16", "2 3000 0 0 100 16", "3 2000 1 1 100 16", "4 2000 1 0 100 33", "5 3000 2 1 100 16",
     "6 3000 2 0 100 121", "7 300 3 1 100 16", "8 300 3 0 100 4", "9 3000 4 1 100 16", "10 3000 4 0 100 16",
@@ -178,19 +180,20 @@ FLAT_CASES = [
 ]
 
 
-@pytest.mark.parametrize("args", FLAT_CASES)
+@pytest.mark.parametrize("args", CONTIG_CASES)
 def test_emulated_contiguous_input_auto(emu_lib, args):
     _run(emu_lib, "contig", args, {"HYEMU_CUS": "2"})
 
 
-@pytest.mark.parametrize("args", CONTIG_CASES)
-def test_emulated_contiguous_input_wave(emu_lib, args):
-    _run(emu_lib, "contig", args, {"HYEMU_CUS": "2", "HYOBFS_KERNEL": "wave"})
+@pytest.mark.parametrize("hashers", ["4", "0"])
+@pytest.mark.parametrize("args", FLAT_CASES)
+def test_emulated_contiguous_input_flat(emu_lib, args, hashers):
+    _run(emu_lib, "contig", args, {"HYEMU_CUS": "2", "HYOBFS_KERNEL": "flat", "HYOBFS_FLAT_HASHERS": hashers})
 
 
 @pytest.mark.parametrize("args", [CONTIG_CASES[i] for i in (1, 2, 10)])
 def test_emulated_contiguous_input_prepass_offsets(emu_lib, args):
-    _run(emu_lib, "contig", args, {"HYEMU_CUS": "2", "HYOBFS_PACKED_RUN_LOG2": "3", "HYOBFS_KERNEL": "wave"})
+    _run(emu_lib, "contig", args, {"HYEMU_CUS": "2", "HYOBFS_PACKED_RUN_LOG2": "3"})
 
 
 # Contiguous input into SLOTS (out_stride > 0): the prepass writes the input offsets

@@ -381,11 +381,11 @@ def test_config3_bimodal_4M_digest(obfs, gpu, golden):
 
 
 # ------------------------------------------- contiguous input: the flat kernel, the wave kernel's length scan
-@pytest.fixture(params=["auto", "wave"])
+@pytest.fixture(params=["auto", "wave", "flat"])
 def contig_obfs(gpu, request):
-    """auto: the flat kernel into packed output from 16-byte aligned input
-    (salamander_flat.h), else the wave kernel; wave: the wave kernel scanning the input
-    lengths with the widths (packed) or the prepass's input offsets (slotted)."""
+    """auto and wave: the wave kernel scanning the input lengths with the widths
+    (packed) or the prepass's input offsets (slotted); flat: the flat kernel into
+    packed output from 16-byte aligned input (salamander_flat.h), else the wave kernel."""
     import hysteria_amd
     o = hysteria_amd.SalamanderObfuscator(PSK, 0)
     o.set_kernel(request.param)
@@ -395,7 +395,7 @@ def contig_obfs(gpu, request):
 
 def _contig_kernel(o, packed=True, aligned=True):
     """The kernel a contiguous-input batch runs under the context's choice."""
-    return "flat" if packed and aligned and o.kernel != "wave" else "wave"
+    return "flat" if packed and aligned and o.kernel == "flat" else "wave"
 
 
 def test_contiguous_bimodal_64k_vs_oracle_and_digest(contig_obfs, gpu, coracle, golden):
@@ -525,7 +525,8 @@ def test_contiguous_input_grid_vs_oracle(contig_obfs, gpu, coracle, case):
     need = hysteria_amd.SalamanderObfuscator.workspace_bytes(inp=src, n=n, **kw)
     want = 2 * tsums + (8 * n if stride else 0)
     if not stride and not mis:   # the flat kernel's tile descriptors (16 KiB tiles)
-        want = max(want, 2 * tsums + 16 + 24 * ((cap + 16383) // 16384 + 1))
+        desc = 16 + 24 * ((cap + 16383) // 16384 + 1)   # + the hashers' key records, 64 B per datagram
+        want = max(want, 2 * tsums + ((desc + 255) // 256) * 256 + 256 + 64 * n)
     assert need == want
     ws = torch.full((need + 64,), 0x3C, dtype=torch.uint8, device=gpu)
     with hysteria_amd.SalamanderObfuscator(psk, 0) as o:   # the case's PSK (the fixture's is average_password)

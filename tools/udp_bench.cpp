@@ -5,7 +5,7 @@
 // Every received payload is checked (sequence number + content tag).
 //
 //   udp_bench [mode=batch|single|raw|coalesce] [pairs=4] [seconds=5] [len=1200] [batch=1024]
-//             [threads=2] [wait_us=50]
+//             [threads=2] [wait_us=50] [rate=0]
 //
 // "raw" sends and receives the same datagrams with plain sendmmsg/recvmmsg and no
 // obfuscation: the loopback socket ceiling.  "single" uses WriteTo/ReadFrom, one
@@ -13,10 +13,15 @@
 // "coalesce" keeps that per-datagram shape (WriteTo / ReadFrom, `threads`
 // writer and `threads` reader threads per pair) on coalescing connections
 // (hyobfs_conn_set_coalescing: GPU batches of up to `batch` behind the calls).
+// rate > 0 offers that many datagrams per second in total (every writer paced to its
+// share: whatever is due is sent, then the writer sleeps): latency at a given load,
+// raw against coalesce; 0 = as fast as the writers go (the saturated rate).
+// Latency = receive time - send-call time of every 64th datagram (p50, p99).
 // Prints one JSON line.
 //   g++ -O2 -std=c++17 tools/udp_bench.cpp -Iinclude -Lhysteria_amd -lhyobfs \
 //       -Wl,-rpath,'$ORIGIN/../hysteria_amd' -lpthread -o tools/udp_bench
 #include <arpa/inet.h>
+#include <sys/prctl.h>
 #include <netinet/in.h>
 #include <string.h>
 #include <sys/socket.h>
@@ -103,6 +108,7 @@ int main(int argc, char** argv) {
     const uint8_t psk[] = "udp_bench_password";
     const int threads = argc > 6 ? atoi(argv[6]) : 2;
     const uint32_t wait_us = argc > 7 ? (uint32_t)atoi(argv[7]) : 50;
+    const double rate = argc > 8 ? atof(argv[8]) : 0.0;   // offered datagrams/s in total, 0 = unpaced
     const bool raw = mode == "raw", coalesce = mode == "coalesce", single = mode == "single" || coalesce;
     if (len < 16 || len > 2040) {
         fprintf(stderr, "len must be in [16, 2040]\n");
@@ -134,6 +140,7 @@ int main(int argc, char** argv) {
       for (int ti = 0; ti < per_side; ++ti) {
         Pair& p = P[pi];
         th.emplace_back([&, pi, ti] {   // sender
+            (void)prctl(PR_SET_TIMERSLACK, 1UL, 0, 0, 0);   // paced writers wake on time
             std::vector<uint8_t> buf((size_t)batch * len);
             std::vector<hyobfs_dgram> d(batch);
             std::vector<mmsghdr> mh(batch);
@@ -151,25 +158,38 @@ int main(int argc, char** argv) {
                 mh[i].msg_hdr.msg_namelen = sizeof p.raddr;
             }
             uint64_t seq = (uint64_t)pi << 48 | (uint64_t)ti << 40;
+            const double share = rate / (double)(pairs * per_side);   // this writer's datagrams/s
+            const uint64_t t_start = now_ns();
+            uint64_t issued = 0;
             while (!stop.load(std::memory_order_relaxed)) {
-                for (uint32_t i = 0; i < batch; ++i) fill(d[i].buf, len, seq++);
+                uint32_t nb = batch;
+                if (share > 0) {   // send what is due by now, up to a batch
+                    const uint64_t want = (uint64_t)((double)(now_ns() - t_start) * share * 1e-9);
+                    if (want <= issued) {
+                        std::this_thread::sleep_for(std::chrono::microseconds(5));
+                        continue;
+                    }
+                    nb = (uint32_t)std::min<uint64_t>(want - issued, batch);
+                    issued += nb;
+                }
+                for (uint32_t i = 0; i < nb; ++i) fill(d[i].buf, len, seq++);
                 if (single) {
-                    for (uint32_t i = 0; i < batch && !stop.load(std::memory_order_relaxed); ++i) {
+                    for (uint32_t i = 0; i < nb && !stop.load(std::memory_order_relaxed); ++i) {
                         stamp(d[i].buf);
                         if (hyobfs_conn_write_to(p.sc, d[i].buf, len, &p.raddr, sizeof p.raddr) > 0) p.sent++;
                     }
                 } else if (raw) {
-                    for (uint32_t i = 0; i < batch; ++i) stamp(d[i].buf);
+                    for (uint32_t i = 0; i < nb; ++i) stamp(d[i].buf);
                     uint32_t done = 0;
-                    while (done < batch) {
-                        int r = sendmmsg(p.sfd, mh.data() + done, batch - done, 0);
+                    while (done < nb) {
+                        int r = sendmmsg(p.sfd, mh.data() + done, nb - done, 0);
                         if (r <= 0) break;
                         done += r;
                     }
                     p.sent += done;
                 } else {
-                    for (uint32_t i = 0; i < batch; ++i) stamp(d[i].buf);
-                    int r = hyobfs_conn_write_batch(p.sc, d.data(), batch);
+                    for (uint32_t i = 0; i < nb; ++i) stamp(d[i].buf);
+                    int r = hyobfs_conn_write_batch(p.sc, d.data(), nb);
                     if (r > 0) p.sent += r;
                 }
             }
@@ -249,11 +269,11 @@ int main(int argc, char** argv) {
         hyobfs_salamander_free(p.rctx);
     }
     const double rx = (double)(r1 - r0), tx = (double)(s1 - s0);
-    printf("{\"mode\": \"%s\", \"pairs\": %d, \"threads_per_side\": %d, \"wait_us\": %u, \"len\": %u, \"batch\": %u, \"seconds\": %.3f, "
+    printf("{\"mode\": \"%s\", \"offered_rate\": %.0f, \"pairs\": %d, \"threads_per_side\": %d, \"wait_us\": %u, \"len\": %u, \"batch\": %u, \"seconds\": %.3f, "
            "\"rx_datagrams_per_s\": %.0f, \"tx_datagrams_per_s\": %.0f, \"rx_payload_GiB_s\": %.4f, "
            "\"tx_payload_GiB_s\": %.4f, \"loss_frac\": %.4f, \"bad\": %llu, \"avg_per_read\": %.1f, "
            "\"latency_us_p50\": %.1f, \"latency_us_p99\": %.1f, \"latency_samples\": %zu}\n",
-           mode.c_str(), pairs, per_side, coalesce ? wait_us : 0u, len, batch, dt, rx / dt, tx / dt, rx * len / dt / (1u << 30), tx * len / dt / (1u << 30),
+           mode.c_str(), rate, pairs, per_side, coalesce ? wait_us : 0u, len, batch, dt, rx / dt, tx / dt, rx * len / dt / (1u << 30), tx * len / dt / (1u << 30),
            sent ? 1.0 - (double)recvd / (double)sent : 0.0, (unsigned long long)bad,
            calls ? (double)recvd / (double)calls : 0.0, pct(0.5), pct(0.99), lat.size());
     return bad ? 1 : 0;
