@@ -9,7 +9,7 @@
 //     copies the datagram and returns len(p).  A flusher thread seals the batch
 //     when it is full, max_wait_us after its first datagram, or once no WriteTo
 //     has added to it for idle_us (the writers paused: a light load does not wait
-//     for max_wait; HYOBFS_COALESCE_IDLE_US, default min(20, max_wait_us)), and launches its
+//     for max_wait; HYOBFS_COALESCE_IDLE_US, default min(100, max_wait_us)), and launches its
 //     obfuscation on the GPU, which reads and writes the batch in place (mapped
 //     pinned memory, gpu_queue_submit); while that kernel runs the thread sends
 //     the PREVIOUS batch with sendmmsg, and the next batch fills.  Three send
@@ -98,14 +98,17 @@ static bool zerocopy_on() {
     static const bool v = env_flag("HYOBFS_COALESCE_ZEROCOPY", true);
     return v;
 }
-// Idle seal (HYOBFS_COALESCE_IDLE_US, default 20): a filling batch no WriteTo has added
+// Idle seal (HYOBFS_COALESCE_IDLE_US, default 100): a filling batch no WriteTo has added
 // to for this long is sealed without waiting for max_wait_us.  Under load the writers
 // arrive far more often and batches still fill; at a light load a datagram waits about
-// this long instead of max_wait_us.
+// this long instead of max_wait_us.  Shorter is not better on a shared host: every
+// batch costs ~25 us of CPU (launch, event, thread wake-ups), and 16 connections
+// sealing every 20 us used the box's whole 16-core CPU share and were throttled
+// (millisecond tails, profiles/r06_host/).
 static uint32_t coalesce_idle_us() {
     static const uint32_t v = [] {
         const char* e = std::getenv("HYOBFS_COALESCE_IDLE_US");
-        const long x = e ? std::atol(e) : 20;
+        const long x = e ? std::atol(e) : 100;
         return (uint32_t)(x < 0 ? 0 : x);
     }();
     return v;

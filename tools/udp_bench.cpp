@@ -22,6 +22,7 @@
 //       -Wl,-rpath,'$ORIGIN/../hysteria_amd' -lpthread -o tools/udp_bench
 #include <arpa/inet.h>
 #include <sys/prctl.h>
+#include <sys/resource.h>
 #include <netinet/in.h>
 #include <string.h>
 #include <sys/socket.h>
@@ -38,6 +39,20 @@
 #include <vector>
 
 #include "../include/hyobfs_conn.h"
+
+// cgroup v2 CPU throttling so far (nr_throttled, throttled_usec), 0 when unreadable
+static void cg_throttle(uint64_t& n, uint64_t& us) {
+    n = us = 0;
+    if (FILE* f = fopen("/sys/fs/cgroup/cpu.stat", "r")) {
+        char k[64];
+        unsigned long long v;
+        while (fscanf(f, "%63s %llu", k, &v) == 2) {
+            if (!strcmp(k, "nr_throttled")) n = v;
+            if (!strcmp(k, "throttled_usec")) us = v;
+        }
+        fclose(f);
+    }
+}
 
 static uint64_t tag(uint64_t seq) { return seq * 0x9E3779B97F4A7C15ull ^ 0xD1B54A32D192ED03ull; }
 
@@ -164,9 +179,12 @@ int main(int argc, char** argv) {
             while (!stop.load(std::memory_order_relaxed)) {
                 uint32_t nb = batch;
                 if (share > 0) {   // send what is due by now, up to a batch
-                    const uint64_t want = (uint64_t)((double)(now_ns() - t_start) * share * 1e-9);
-                    if (want <= issued) {
-                        std::this_thread::sleep_for(std::chrono::microseconds(5));
+                    const uint64_t now = now_ns();
+                    const uint64_t want = (uint64_t)((double)(now - t_start) * share * 1e-9);
+                    if (want <= issued) {   // sleep until the next datagram is due (few wakeups)
+                        const double next_ns = (double)(issued + 1) / share * 1e9 + (double)t_start;
+                        const double gap = next_ns - (double)now;
+                        std::this_thread::sleep_for(std::chrono::nanoseconds((int64_t)std::max(gap, 2000.0)));
                         continue;
                     }
                     nb = (uint32_t)std::min<uint64_t>(want - issued, batch);
@@ -243,6 +261,10 @@ int main(int argc, char** argv) {
 
     // warm up 0.5 s, then count over the timed window
     std::this_thread::sleep_for(std::chrono::milliseconds(500));
+    uint64_t thr_n0, thr_us0, thr_n1, thr_us1;
+    cg_throttle(thr_n0, thr_us0);
+    rusage ru0{}, ru1{};
+    getrusage(RUSAGE_SELF, &ru0);
     uint64_t r0 = 0, s0 = 0;
     for (auto& p : P) r0 += p.recvd, s0 += p.sent;
     const auto t0 = std::chrono::steady_clock::now();
@@ -250,6 +272,10 @@ int main(int argc, char** argv) {
     uint64_t r1 = 0, s1 = 0;
     for (auto& p : P) r1 += p.recvd, s1 += p.sent;
     const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    getrusage(RUSAGE_SELF, &ru1);
+    cg_throttle(thr_n1, thr_us1);
+    auto tv_s = [](const timeval& t) { return (double)t.tv_sec + 1e-6 * (double)t.tv_usec; };
+    const double cpu_s = tv_s(ru1.ru_utime) - tv_s(ru0.ru_utime) + tv_s(ru1.ru_stime) - tv_s(ru0.ru_stime);
     stop = true;
     std::this_thread::sleep_for(std::chrono::milliseconds(400));
     rstop = true;
@@ -272,9 +298,11 @@ int main(int argc, char** argv) {
     printf("{\"mode\": \"%s\", \"offered_rate\": %.0f, \"pairs\": %d, \"threads_per_side\": %d, \"wait_us\": %u, \"len\": %u, \"batch\": %u, \"seconds\": %.3f, "
            "\"rx_datagrams_per_s\": %.0f, \"tx_datagrams_per_s\": %.0f, \"rx_payload_GiB_s\": %.4f, "
            "\"tx_payload_GiB_s\": %.4f, \"loss_frac\": %.4f, \"bad\": %llu, \"avg_per_read\": %.1f, "
-           "\"latency_us_p50\": %.1f, \"latency_us_p99\": %.1f, \"latency_samples\": %zu}\n",
+           "\"latency_us_p50\": %.1f, \"latency_us_p99\": %.1f, \"latency_samples\": %zu, "
+           "\"cpu_cores_used\": %.2f, \"cgroup_throttled_periods\": %llu, \"cgroup_throttled_ms\": %.1f}\n",
            mode.c_str(), rate, pairs, per_side, coalesce ? wait_us : 0u, len, batch, dt, rx / dt, tx / dt, rx * len / dt / (1u << 30), tx * len / dt / (1u << 30),
            sent ? 1.0 - (double)recvd / (double)sent : 0.0, (unsigned long long)bad,
-           calls ? (double)recvd / (double)calls : 0.0, pct(0.5), pct(0.99), lat.size());
+           calls ? (double)recvd / (double)calls : 0.0, pct(0.5), pct(0.99), lat.size(), cpu_s / dt,
+           (unsigned long long)(thr_n1 - thr_n0), (double)(thr_us1 - thr_us0) / 1e3);
     return bad ? 1 : 0;
 }
