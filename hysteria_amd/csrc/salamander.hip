@@ -320,7 +320,6 @@ static hipError_t launch_contiguous(BatchParams& bp, const KeyParams& k, hipStre
         F.out_total = bp.tile_sums + ntiles;     // the width scan's total
         F.in_total = bp.in_tile_sums + ntiles;   // the length scan's total
         F.ntiles_max = flat_ntiles_max(bp.out_cap);
-        F.t0 = 0;
         F.krec = reinterpret_cast<uint8_t*>((reinterpret_cast<uintptr_t>(F.cut) + flat_desc_bytes(bp.out_cap) + 255) &
                                             ~(uintptr_t)255);
         F.epoch = next_epoch();

@@ -78,7 +78,6 @@ struct FlatParams {
     uint64_t ntiles_max;
     const uint64_t* in_total;    // input bytes: the length scan's total (device)
     const uint64_t* out_total;   // the width scan's total: the valid output's end without a cut
-    uint64_t t0;        // unused (one launch)
     uint8_t* krec;      // key records: per datagram 4 granules {key word, epoch} (krec_*)
     uint64_t epoch;     // this call's tag (never 0)
     uint32_t nhash;     // hasher workgroups in front of the tile workgroups

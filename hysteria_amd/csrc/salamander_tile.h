@@ -325,6 +325,8 @@ __global__ __launch_bounds__(256, HY_TILE_MIN_WAVES) void salamander_tile_kernel
         const uint64_t kw = quad_key<SW>(K, salt, qi);
 #if HY_TILE_PREFETCH && !defined(HYOBFS_EMULATE)
         asm volatile("" ::"v"(pf));
+#elif HY_TILE_PREFETCH
+        hyemu_sink(pf);   // the emulated tier performs the load too: ASan checks its address
 #endif
         if (qk < nt) {
             s_key[qk * 8 + qi] = kw;

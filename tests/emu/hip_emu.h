@@ -206,6 +206,11 @@ inline unsigned long long atomicMax(unsigned long long* p, unsigned long long v)
     hyemu::launch(dim3(grid), dim3(block), (size_t)(shmem), [&] { kernel(__VA_ARGS__); })
 inline bool hyemu_readable(const void* p) { return !__asan_address_is_poisoned(p); }
 inline uint8_t* hyemu_dyn_lds() { return hyemu::g_ctx.dyn.get(); }
+// keeps a load whose value the kernel discards (a prefetch) from being optimised away
+inline void hyemu_sink(uint32_t v) {
+    static volatile uint32_t s;
+    s = v;
+}
 
 // ---- runtime API subset
 inline hipError_t hipGetLastError() { return hipSuccess; }

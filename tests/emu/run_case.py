@@ -182,13 +182,23 @@ def case_uniform(n, L, obf):
             len_uniform=L + 8)
 
 
-def case_slotted(n, L, obf, slot_pad, in_pad, psk_len):
+def case_slotted(n, L, obf, slot_pad, in_pad, psk_len, exact=0):
     """Uniform lengths into slots of W + slot_pad bytes (gap bytes must stay
-    untouched), inputs at a stride of L + in_pad, a PSK of psk_len bytes."""
+    untouched), inputs at a stride of L + in_pad, a PSK of psk_len bytes.  exact=1:
+    the input buffer ends right after the last datagram's L bytes ((n-1) stride + L,
+    the API's promise; ASan reports any read past it, e.g. the tile kernel's prefetch
+    of a short datagram in a long slot)."""
     psk = bytes((7 * i + 1) & 0xFF for i in range(psk_len))
     W = L + 8 if obf else L - 8
     stride, istride = W + slot_pad, L + in_pad
-    inp = np.frombuffer(ref.stream_bytes(1, 0, n * istride + 16), np.uint8).copy()
+    if exact:
+        size = (n - 1) * istride + L
+        raw = np.empty(size + 15, np.uint8)
+        off = (-raw.ctypes.data) % 16   # 16-byte aligned start (the tile kernel's condition)
+        inp = raw[off:off + size]
+        inp[:] = np.frombuffer(ref.stream_bytes(1, 0, size), np.uint8)
+    else:
+        inp = np.frombuffer(ref.stream_bytes(1, 0, n * istride + 16), np.uint8).copy()
     salts = ref.splitmix64_array(2, 0, n)
     run(obf, psk, None, None, inp, salts, n * stride, out_stride=stride, in_stride=istride, len_uniform=L)
 
@@ -411,7 +421,7 @@ if __name__ == "__main__":
     elif which == "pcap":
         case_packed_cap(*args[:3], bool(args[3]), args[4], args[5])
     elif which == "slotted":
-        case_slotted(args[0], args[1], bool(args[2]), args[3], args[4], args[5])
+        case_slotted(args[0], args[1], bool(args[2]), args[3], args[4], args[5], args[6] if len(args) > 6 else 0)
     elif which == "uniform":
         case_uniform(args[0], args[1], bool(args[2]))
     elif which == "host":

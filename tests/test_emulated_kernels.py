@@ -36,6 +36,7 @@ def emu_lib():
 SPECS = {
     "test_emulated_packed_auto": lambda p: (p["which"], p["args"], {"HYEMU_CUS": "2"}),
     "test_emulated_tile_kernel": lambda p: (p["which"], p["args"], {"HYOBFS_KERNEL": "tile", "HYEMU_CUS": "2"}),
+    "test_emulated_tile_kernel_exact_input": lambda p: ("slotted", p["args"], {"HYOBFS_KERNEL": "tile", "HYEMU_CUS": "2"}),
     "test_emulated_wave_kernel_forced": lambda p: None if p["which"] in ("conn", "host", "coalesce", "quic",
                                                                          "lifecycle", "deadline", "closerace") else (
         p["which"], p["args"], {"HYEMU_CUS": p["cus"], "HYOBFS_KERNEL": "wave"}),
@@ -232,6 +233,15 @@ from tile_cases import TILE_CASES  # noqa: E402  (the tile kernel's layout grid,
 @pytest.mark.parametrize("which,args", TILE_CASES)
 def test_emulated_tile_kernel(emu_lib, which, args):
     _run(emu_lib, which, args, {"HYOBFS_KERNEL": "tile", "HYEMU_CUS": "2"})
+
+
+# Short datagrams in long input slots, the input buffer ending right after the last
+# datagram's L bytes ((n-1) x stride + L, all the API promises): the tile kernel's
+# obfuscate prefetch loads (salamander_tile.h, HY_TILE_PREFETCH) stay inside each
+# datagram, ASan reports any byte read past the buffer.
+@pytest.mark.parametrize("args", ["40 16 1 8 4080 16 1", "40 24 0 8 4072 16 1", "33 1200 1 0 2896 16 1"])
+def test_emulated_tile_kernel_exact_input(emu_lib, args):
+    _run(emu_lib, "slotted", args, {"HYOBFS_KERNEL": "tile", "HYEMU_CUS": "2"})
 
 
 # A batch split into several launches (salamander_tile.h launch_tile_sw: big batches

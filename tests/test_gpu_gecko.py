@@ -18,7 +18,7 @@ KEY, NONCE = bytes(range(7, 39)), bytes(range(100, 112))   # explicit pad keystr
 
 def _dev(a, gpu):
     import torch
-    return torch.from_numpy(np.ascontiguousarray(a).view(np.uint8)).to(gpu)
+    return torch.from_numpy(np.array(a, copy=True).view(np.uint8)).to(gpu)   # writable copy (torch warns on read-only arrays)
 
 
 def _messages(n, seed):
