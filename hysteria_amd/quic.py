@@ -225,7 +225,7 @@ def _pack(packets):
 
 def _to(dev, a):
     import torch
-    return torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    return torch.from_numpy(np.array(a, copy=True)).to(dev)   # writable copy (torch warns on read-only arrays)
 
 
 def _records(t, dtype):
