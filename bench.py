@@ -254,6 +254,12 @@ def main():
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(spawn_ranks(args))
 
+    # stdout carries exactly one JSON line: whatever libraries print (gloo's "Rank r is
+    # connected to ..." lines) goes to stderr until the line is printed
+    sys.stdout.flush()
+    real_stdout = os.dup(1)
+    os.dup2(2, 1)
+
     import torch
     import torch.distributed as dist
     import hysteria_amd as hy
@@ -434,6 +440,9 @@ def main():
         res["cpu_baseline"] = cpu_baseline(1200, args.cpu_seconds)
     elif rank == 0:
         res["cpu_baseline"] = None
+    sys.stdout.flush()
+    os.dup2(real_stdout, 1)
+    os.close(real_stdout)
     if rank == 0:
         print(json.dumps(res), flush=True)
     obfs.close()

@@ -629,14 +629,12 @@ int64_t coalescer_write(Coalescer* q, const uint8_t* p, size_t len, const void* 
 int64_t coalescer_read(Coalescer* q, uint8_t* p, size_t cap, void* addr, uint32_t* addrlen) {
     CallerGuard g(q);
     // SetReadDeadline: the connection's absolute read deadline if one is set
-    // (re-read whenever it changes), else SO_RCVTIMEO read once, one absolute
-    // deadline for the whole call
-    timeval tv{0, 0};
-    socklen_t tl = sizeof tv;
-    (void)getsockopt(q->fd, SOL_SOCKET, SO_RCVTIMEO, &tv, &tl);
-    const auto t = std::chrono::seconds(tv.tv_sec) + std::chrono::microseconds(tv.tv_usec);
-    const bool timed = t.count() != 0;
-    const Clock::time_point deadline = Clock::now() + t;
+    // (re-read whenever it changes), else SO_RCVTIMEO, read when the call first has
+    // to wait (a datagram already queued costs no system call): one absolute deadline
+    // for the whole call
+    const Clock::time_point start = Clock::now();
+    bool have_to = false, timed = false;
+    Clock::time_point deadline{};
     for (;;) {
         int bi;
         uint32_t idx;
@@ -657,6 +655,15 @@ int64_t coalescer_read(Coalescer* q, uint8_t* p, size_t cap, void* addr, uint32_
                     return -1;
                 }
                 auto woken = [&] { return !q->ready.empty() || q->rx_err || q->rx_fatal || q->stop; };
+                if (!have_to) {
+                    timeval tv{0, 0};
+                    socklen_t tl = sizeof tv;
+                    (void)getsockopt(q->fd, SOL_SOCKET, SO_RCVTIMEO, &tv, &tl);
+                    const auto t = std::chrono::seconds(tv.tv_sec) + std::chrono::microseconds(tv.tv_usec);
+                    timed = t.count() != 0;
+                    deadline = start + t;
+                    have_to = true;
+                }
                 if (q->dl->read.load(std::memory_order_acquire)) {
                     if (!wait_deadline(q->cv_ready, lk, q->dl->read, woken)) {
                         errno = EAGAIN;

@@ -183,3 +183,33 @@ def test_gpu_rank_processes_product_shards(tmp_path, world):
     n = 200_000
     _run_ranks("gpu", n, tmp_path, world=world, timeout=110)
     assert (tmp_path / "joined.bin").read_bytes() == _oracle_whole(n)
+
+
+def test_n_gt_1_bench_line_is_self_contained():
+    """The N > 1 bench line the driver's 8-GPU run prints, as a one-card --gpus 2
+    rehearsal on the final sources recorded it (profiles/r06_final/): BASELINE's metric,
+    weak scaling over configs[3]'s 8M-datagram shard per rank, the roofline with the PMC
+    traffic of that shard (profiles/pmc_traffic.json, keyed by the build id), every rank's
+    PCI bus id and call time, the shared-card flag, and no CPU baseline (rank 0 at N = 1
+    only).  Every key the driver and the judge read is checked."""
+    import json
+    ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    line = json.loads(open(os.path.join(ROOT, "profiles", "r06_final", "bench_n2_one_gpu_rehearsal.json")).read())
+    base = json.load(open(os.path.join(ROOT, "BASELINE.json")))
+    assert line["metric"] == base["metric"] and line["unit"] == "GiB/s" and line["higher_is_better"] is True
+    assert line["n_gpus"] == 2 and line["scaling"] == "weak" and line["value"] > 0 and line["ms_per_step"] > 0
+    assert line["steps"] > 0 and line["warmup"] >= 0 and line["vs_baseline"] is None and line["dtype"] == "u8"
+    cfg = line["config"]
+    assert cfg["datagrams_per_gpu"] == 1 << 23 and cfg["global_datagrams"] == 2 << 23 and cfg["datagram_len"] == 1200
+    roof = line["roofline"]
+    assert roof["bound"] == "hbm" and roof["unit"] == "GB/s" and roof["peak"] == 8000.0
+    assert roof["traffic"] and roof["traffic_over_algorithmic"] < 1.05   # the 8M shard's PMC entry
+    assert roof["kernel_src_sha"] == roof["lib_build_id"]
+    assert abs(roof["frac"] - roof["achieved"] / roof["peak"]) < 1e-3
+    assert roof["algorithmic_bytes_per_launch"] == (1 << 23) * (2 * 1200 + 16)
+    ranks = line["ranks"]
+    assert [r["rank"] for r in ranks] == [0, 1]
+    assert all(len(r["pci_bus_id"]) >= 12 and r["obf_call_ms"] > 0 for r in ranks)
+    assert line["devices_shared"] is True   # the rehearsal ran both ranks on one card
+    assert line["cpu_baseline"] is None and len(line["per_gpu_GiBs"]) == 2
+    assert "deobfuscate" in line and line["deobfuscate"]["frac"] > 0
