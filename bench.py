@@ -50,18 +50,13 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md); 6.29 TB/s measured float4 copy
 PSK = b"average_password"
 METRIC = "device-resident packet-obfs GiB/s @ 1200B datagrams, 1/2/4/8 MI355X"
-# the obfuscate kernel each workload runs, per --kernel (rocprof names in profiles/)
 BIMODAL_MIN_WARMUP = 20
 WARM_LOAD_MS = 60.0   # the fixed warm load before a workload's timed legs (>= 20 ms, see above)
-KERNEL_NAMES = {
-    "uniform": {"auto": "salamander_tile_kernel<obfuscate> (salamander_tile.h)",
-                "tile": "salamander_tile_kernel<obfuscate> (salamander_tile.h)",
-                "flat": "salamander_tile_kernel<obfuscate> (salamander_tile.h)",
+KERNEL_NAMES = {   # keyed by the kernel the library reports for the batch (hyobfs_salamander_batch_kernel)
+    "uniform": {"tile": "salamander_tile_kernel<obfuscate> (salamander_tile.h)",
                 "wave": "salamander_wave_kernel<obfuscate, slotted> (salamander_wave.h)"},
-    "bimodal": {"auto": "salamander_flat_kernel<obfuscate> (salamander_flat.h) + width/length scan and locate prepass (3 launches)",
-                "tile": "salamander_flat_kernel<obfuscate> (salamander_flat.h) + width/length scan and locate prepass (3 launches)",
-                "flat": "salamander_flat_kernel<obfuscate> (salamander_flat.h) + width/length scan and locate prepass (3 launches)",
-                "wave": "salamander_wave_kernel<obfuscate, packed> (salamander_wave.h) + width/length scan (2 launches)"},
+    "bimodal": {"wave": "salamander_wave_kernel<obfuscate, packed> (salamander_wave.h) + width/length sums and scan (3 launches)",
+                "flat": "salamander_flat_kernel<obfuscate> (salamander_flat.h) + width/length sums, scan and locate (4 launches)"},
 }
 
 
@@ -89,7 +84,9 @@ def kernel_src_sha() -> str:
     return src_sha()
 
 
-def pmc_traffic(workload: str, direction: str, datagrams: int, length) -> dict | None:
+def pmc_traffic(workload: str, direction: str, datagrams: int, length, kernel: str) -> dict | None:
+    """The committed PMC traffic entry for this batch, if one was measured on these kernel
+    sources with the same kernel choice (kernel = "tile" / "wave" / "flat")."""
     f = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         entries = json.load(open(f)).get("entries", [])
@@ -101,7 +98,8 @@ def pmc_traffic(workload: str, direction: str, datagrams: int, length) -> dict |
         return None
     for e in entries:
         if (e.get("src_sha") == sha and e.get("workload") == workload and e.get("direction") == direction
-                and e.get("datagrams") == datagrams and e.get("len") == length):
+                and e.get("datagrams") == datagrams and e.get("len") == length
+                and f"salamander_{kernel}_kernel<" in e.get("kernel", "")):
             return e
     return None
 
@@ -201,8 +199,9 @@ def setup_uniform(hy, obfs, dev, P, L, first):
     def step_deobf():
         obfs.deobfuscate_batch(wire, P, in_stride=L + 8, len_uniform=L + 8, out=back, out_stride=L)
 
+    kernel = obfs.batch_kernel(True, inp=inp, n=P, in_stride=L, len_uniform=L, out=wire, out_stride=L + 8)
     return dict(obf=step_obf, deobf=step_deobf, payload=P * L, obf_bytes=P * (2 * L + 16),
-                deobf_bytes=P * (2 * L + 8), inp=inp, wire=wire, back=back, n=P, len=L)
+                deobf_bytes=P * (2 * L + 8), inp=inp, wire=wire, back=back, n=P, len=L, kernel=kernel)
 
 
 def setup_bimodal(hy, obfs, dev, P, first):
@@ -245,8 +244,10 @@ def setup_bimodal(hy, obfs, dev, P, first):
         obfs.deobfuscate_batch(wire, P, in_len=out_len, out=back, out_cap=total_in,
                                workspace=ws, workspace_bytes=ws.numel())
 
+    kernel = obfs.batch_kernel(True, inp=inp, n=P, in_len=lens, out=wire, out_cap=cap)
     return dict(obf=step_obf, deobf=step_deobf, payload=total_in, obf_bytes=2 * total_in + 16 * P,
-                deobf_bytes=2 * total_in + 8 * P, inp=inp, wire=wire, back=back, n=P, len="bimodal")
+                deobf_bytes=2 * total_in + 8 * P, inp=inp, wire=wire, back=back, n=P, len="bimodal",
+                kernel=kernel)
 
 
 def main():
@@ -344,10 +345,10 @@ def main():
         total_payload = w["payload"] * world * args.steps   # every step processes the whole batch
         achieved = w["obf_bytes"] / ev_obf / 1e9
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None, "kernel": KERNEL_NAMES[workload][args.kernel],
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None, "kernel": KERNEL_NAMES[workload].get(w["kernel"], w["kernel"]),
                 "algorithmic_bytes_per_launch": w["obf_bytes"], "avg_launch_ms": round(ev_obf * 1e3, 4),
                 "kernel_src_sha": kernel_src_sha(), "lib_build_id": hy.build_id()}
-        t = pmc_traffic(workload, "obfuscate", w["n"], w["len"])
+        t = pmc_traffic(workload, "obfuscate", w["n"], w["len"], w["kernel"])
         if t:
             roof["traffic"] = t["hbm_bytes_per_launch"]
             roof["traffic_over_algorithmic"] = round(t["hbm_bytes_per_launch"] / w["obf_bytes"], 4)
@@ -357,7 +358,7 @@ def main():
                 "achieved_GBs": round(w["deobf_bytes"] / ev_deobf / 1e9, 1),
                 "frac": round(w["deobf_bytes"] / ev_deobf / 1e9 / HBM_PEAK_GBS, 4),
                 "avg_launch_ms": round(ev_deobf * 1e3, 4), "algorithmic_bytes_per_launch": w["deobf_bytes"]}
-        t = pmc_traffic(workload, "deobfuscate", w["n"], w["len"])
+        t = pmc_traffic(workload, "deobfuscate", w["n"], w["len"], w["kernel"])
         if t:
             deob["traffic"] = t["hbm_bytes_per_launch"]
             deob["traffic_over_algorithmic"] = round(t["hbm_bytes_per_launch"] / w["deobf_bytes"], 4)

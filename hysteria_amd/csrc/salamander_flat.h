@@ -17,10 +17,11 @@
 //     1. every wave issues its rows of the window's LDS-DMA (global_load_lds_dwordx4,
 //        non-temporal, 1 KiB per wave instruction) first, so the copy is in flight
 //        during everything else;
-//     2. every wave loads the lengths and salts of the tile's datagrams (lane per
-//        datagram) and scans them (32-bit, tile-relative); wave w hashes the keys of
-//        datagrams 16w .. 16w + 15 four lanes per key (quad_key, salamander_tile.h),
-//        rotated to the output's 32-byte phase; wave 0 writes the table;
+//     2. wave 0 loads the lengths and salts of the tile's datagrams (lane per
+//        datagram), scans them (32-bit, tile-relative) and takes their keys from the
+//        key records the launch's hasher workgroups write (flat_hasher, one lane per
+//        key; a record not yet written after a bounded wait is hashed in place, four
+//        lanes per key), rotated to the output's 32-byte phase, into the table;
 //     3. one barrier, then every thread composes four 16-byte output chunks:
 //        * inside one payload (the common case): two 8-byte LDS reads of the stage --
 //          with contiguous input the stage offset of a datagram's payload is a
@@ -93,7 +94,7 @@ inline uint64_t flat_workspace_bytes(uint64_t out_cap, uint64_t n) {
 }
 
 // Hasher workgroups per launch (HYOBFS_FLAT_HASHERS overrides; 0: every tile hashes its
-// own keys).  64 x 4 waves hash configs[2]'s 4M keys in ~0.9 ms, ahead of the tiles.
+// own keys).  They are the launch's first workgroups, so they start ahead of the tiles.
 #ifndef HY_FLAT_HASHERS
 #define HY_FLAT_HASHERS 256
 #endif
@@ -213,8 +214,7 @@ struct FlatLDS {
 };
 
 // The helpers below take any LDS layout with the fields of FlatLDS (stage with kFGuard
-// bytes on both sides, key, salt, o, dlt, w): the flat kernel's and the group kernel's
-// (salamander_group.h).
+// bytes on both sides, key, salt, o, dlt, w).
 // 16 bytes of the stage from stage index q (>= -kFGuard, < stage bytes + kFGuard - 16)
 template <class LDS>
 __device__ __forceinline__ u128 flat_stage16(const LDS& S, int32_t q) {
