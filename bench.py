@@ -199,7 +199,7 @@ def setup_uniform(hy, obfs, dev, P, L, first):
     def step_deobf():
         obfs.deobfuscate_batch(wire, P, in_stride=L + 8, len_uniform=L + 8, out=back, out_stride=L)
 
-    kernel = obfs.batch_kernel(True, inp=inp, n=P, in_stride=L, len_uniform=L, out=wire, out_stride=L + 8)
+    kernel = obfs.batch_kernel(True, inp=inp, n=P, in_stride=L, len_uniform=L, salts=salts, out=wire, out_stride=L + 8)
     return dict(obf=step_obf, deobf=step_deobf, payload=P * L, obf_bytes=P * (2 * L + 16),
                 deobf_bytes=P * (2 * L + 8), inp=inp, wire=wire, back=back, n=P, len=L, kernel=kernel)
 
@@ -244,7 +244,8 @@ def setup_bimodal(hy, obfs, dev, P, first):
         obfs.deobfuscate_batch(wire, P, in_len=out_len, out=back, out_cap=total_in,
                                workspace=ws, workspace_bytes=ws.numel())
 
-    kernel = obfs.batch_kernel(True, inp=inp, n=P, in_len=lens, out=wire, out_cap=cap)
+    kernel = obfs.batch_kernel(True, inp=inp, n=P, in_len=lens, salts=salts, out=wire, out_cap=cap,
+                               out_off=out_off, out_len=out_len, workspace=ws, workspace_bytes=ws.numel())
     return dict(obf=step_obf, deobf=step_deobf, payload=total_in, obf_bytes=2 * total_in + 16 * P,
                 deobf_bytes=2 * total_in + 8 * P, inp=inp, wire=wire, back=back, n=P, len="bimodal",
                 kernel=kernel)

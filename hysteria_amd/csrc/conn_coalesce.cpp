@@ -504,11 +504,17 @@ Coalescer* coalescer_new(int fd, hyobfs_salamander* ctx, uint32_t max_batch, uin
         return nullptr;
     }
     for (int i = 0; i < Coalescer::kRx; ++i) q->freelist.push_back(i);
+    // named threads: per-thread CPU use is attributable (tools/udp_bench, top -H)
     q->flusher = std::thread([q] {
-        (void)prctl(PR_SET_TIMERSLACK, 1UL, 0, 0, 0);   // wake at the idle point, not up to 50 us later
+        (void)prctl(PR_SET_NAME, "hyobfs-tx", 0, 0, 0);
+        (void)prctl(PR_SET_TIMERSLACK, 1UL, 0, 0, 0);   // wake at the idle point (and from gpu_queue_wait's sleeps) on time
         q->flush_loop();
     });
-    q->reader = std::thread([q] { q->read_loop(); });
+    q->reader = std::thread([q] {
+        (void)prctl(PR_SET_NAME, "hyobfs-rx", 0, 0, 0);
+        (void)prctl(PR_SET_TIMERSLACK, 1UL, 0, 0, 0);   // gpu_queue_wait's short sleeps end on time
+        q->read_loop();
+    });
     return q;
 }
 

@@ -14,6 +14,7 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <thread>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -589,11 +590,7 @@ GpuQueue* gpu_queue_new(hyobfs_salamander* c) {
     if (!q) return nullptr;
     q->ctx = c;
     bool ok = hipStreamCreateWithFlags(&q->s, hipStreamNonBlocking) == hipSuccess;
-    // blocking sync: a coalescer thread waiting for its batch sleeps instead of spinning
-    // (16 connections' threads spinning on one box's CPU share throttled every thread:
-    // millisecond latency tails); HYOBFS_COALESCE_SPIN=1 spins
-    const unsigned fl = hipEventDisableTiming | (coalesce_spin() ? 0u : (unsigned)hipEventBlockingSync);
-    for (auto& e : q->ev) ok = ok && hipEventCreateWithFlags(&e, fl) == hipSuccess;
+    for (auto& e : q->ev) ok = ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
     if (!ok) {
         gpu_queue_free(q);
         return nullptr;
@@ -618,8 +615,22 @@ int gpu_queue_submit(GpuQueue* q, const hyobfs_batch* b, bool obf, int slot) {
     return hipEventRecord(q->ev[slot & 3], q->s) == hipSuccess ? HYOBFS_OK : HYOBFS_ERR_HIP;
 }
 
+// Waits for the slot's batch by sleeping between event queries.  hipEventSynchronize
+// busy-waits here even on a blocking-sync event: with 16 connections' streams sharing the
+// GPU's hardware queues a batch takes ~100 us, and the coalescer threads spent that much
+// CPU per batch spinning -- 12 of the box's 16 cores at half load (a phase probe,
+// tools/ab_patches/coalesce_cpu_probe.patch).  A GPU step takes >= ~18 us,
+// so the first query comes after 8 us and the later ones every 8-16 us: a few us of CPU
+// per batch and at most ~16 us of added latency.  HYOBFS_COALESCE_SPIN=1 spins instead.
 int gpu_queue_wait(GpuQueue* q, int slot) {
-    return hipEventSynchronize(q->ev[slot & 3]) == hipSuccess ? HYOBFS_OK : HYOBFS_ERR_HIP;
+    hipEvent_t e = q->ev[slot & 3];
+    if (coalesce_spin()) return hipEventSynchronize(e) == hipSuccess ? HYOBFS_OK : HYOBFS_ERR_HIP;
+    for (uint32_t us = 8;; us = us < 16 ? us * 2 : 16) {
+        const hipError_t r = hipEventQuery(e);
+        if (r == hipSuccess) return HYOBFS_OK;
+        if (r != hipErrorNotReady) return HYOBFS_ERR_HIP;
+        std::this_thread::sleep_for(std::chrono::microseconds(us));
+    }
 }
 
 }  // namespace hyobfs

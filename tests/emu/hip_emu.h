@@ -53,7 +53,7 @@ inline uint4 make_uint4(uint32_t a, uint32_t b, uint32_t c, uint32_t d) { return
 typedef int hipError_t;
 typedef void* hipStream_t;
 typedef void* hipEvent_t;
-enum { hipSuccess = 0, hipErrorInvalidValue = 1, hipErrorOutOfMemory = 2 };
+enum { hipSuccess = 0, hipErrorInvalidValue = 1, hipErrorOutOfMemory = 2, hipErrorNotReady = 600 };
 enum { hipHostMallocMapped = 2, hipStreamNonBlocking = 1 };
 enum hipDeviceAttribute_t { hipDeviceAttributeMultiprocessorCount = 0 };
 struct hipDeviceProp_t {
@@ -237,7 +237,7 @@ inline hipError_t hipStreamCreateWithFlags(hipStream_t* s, unsigned) { *s = (hip
 inline hipError_t hipStreamDestroy(hipStream_t) { return hipSuccess; }
 enum { hipEventDisableTiming = 2, hipEventBlockingSync = 1 };
 // Events are numbered in creation order (1, 2, ...).  Fault injection for the CPU tier:
-// HYEMU_FAIL_EVENTS_FROM=k makes hipEventSynchronize fail for every event numbered k or
+// HYEMU_FAIL_EVENTS_FROM=k makes hipEventSynchronize / hipEventQuery fail for every event numbered k or
 // later (a coalescing connection's send queue creates events 1-4 and its receive queue
 // 5-8 in a fresh process: k = 5 fails exactly the receive side's GPU steps).
 namespace hyemu {
@@ -255,6 +255,8 @@ inline hipError_t hipEventSynchronize(hipEvent_t e) {
     static const uintptr_t from = (uintptr_t)hyemu::env_int("HYEMU_FAIL_EVENTS_FROM", 0);
     return from && (uintptr_t)e >= from ? hipErrorInvalidValue : hipSuccess;
 }
+// launches run synchronously: an event is complete when queried (or failed, as above)
+inline hipError_t hipEventQuery(hipEvent_t e) { return hipEventSynchronize(e); }
 enum hipMemoryType { hipMemoryTypeUnregistered = 0, hipMemoryTypeHost = 1, hipMemoryTypeDevice = 2 };
 struct hipPointerAttribute_t {
     hipMemoryType type;

@@ -14,11 +14,11 @@
 // writer and `threads` reader threads per pair) on coalescing connections
 // (hyobfs_conn_set_coalescing: GPU batches of up to `batch` behind the calls).
 // rate > 0 offers that many datagrams per second in total (every writer paced to its
-// share: whatever is due is sent, then the writer sleeps): latency at a given load,
+// share: whatever is due is sent, then the writer sleeps, at least 20 us): latency at a given load,
 // raw against coalesce; 0 = as fast as the writers go (the saturated rate).
 // Latency = receive time - send-call time of every 64th datagram (p50, p99).
 // Prints one JSON line.
-//   g++ -O2 -std=c++17 tools/udp_bench.cpp -Iinclude -Lhysteria_amd -lhyobfs \
+//   g++ -O2 -std=c++17 tools/udp_bench.cpp -Iinclude -Lhysteria_amd -lhyobfs
 //       -Wl,-rpath,'$ORIGIN/../hysteria_amd' -lpthread -o tools/udp_bench
 #include <arpa/inet.h>
 #include <sys/prctl.h>
@@ -26,10 +26,14 @@
 #include <netinet/in.h>
 #include <string.h>
 #include <sys/socket.h>
+#include <sys/syscall.h>
+#include <dirent.h>
 #include <unistd.h>
 
 #include <algorithm>
 #include <atomic>
+#include <map>
+#include <set>
 #include <mutex>
 #include <chrono>
 #include <cstdio>
@@ -53,6 +57,45 @@ static void cg_throttle(uint64_t& n, uint64_t& us) {
         fclose(f);
     }
 }
+
+// CPU time (utime + stime, clock ticks) and name of every thread of this process
+struct TaskCpu {
+    std::string comm;
+    uint64_t ticks;
+};
+static std::map<int, TaskCpu> task_cpu() {
+    std::map<int, TaskCpu> m;
+    DIR* d = opendir("/proc/self/task");
+    if (!d) return m;
+    while (dirent* e = readdir(d)) {
+        const int tid = atoi(e->d_name);
+        if (tid <= 0) continue;
+        char path[64], line[1024];
+        snprintf(path, sizeof path, "/proc/self/task/%d/stat", tid);
+        FILE* f = fopen(path, "r");
+        if (!f) continue;
+        const size_t n = fread(line, 1, sizeof line - 1, f);
+        fclose(f);
+        line[n] = 0;
+        char* l = strchr(line, '(');
+        char* r = strrchr(line, ')');
+        if (!l || !r) continue;
+        TaskCpu t{std::string(l + 1, r), 0};
+        // fields after the comm: state(3) ... utime(14) stime(15)
+        unsigned long long ut = 0, st = 0;
+        int field = 3;
+        for (char* q = strtok(r + 2, " "); q; q = strtok(nullptr, " "), ++field) {
+            if (field == 14) ut = strtoull(q, nullptr, 10);
+            if (field == 15) { st = strtoull(q, nullptr, 10); break; }
+        }
+        t.ticks = ut + st;
+        m[tid] = t;
+    }
+    closedir(d);
+    return m;
+}
+
+constexpr double kMinSleepNs = 20000.0;   // a paced writer's shortest sleep
 
 static uint64_t tag(uint64_t seq) { return seq * 0x9E3779B97F4A7C15ull ^ 0xD1B54A32D192ED03ull; }
 
@@ -150,12 +193,19 @@ int main(int argc, char** argv) {
 
     std::atomic<bool> stop{false}, rstop{false};
     std::vector<std::thread> th;
+    std::mutex tid_mu;
+    std::set<int> writer_tids, reader_tids;   // the bench's own threads (CPU breakdown)
+    auto note_tid = [&](std::set<int>& s) {
+        std::lock_guard<std::mutex> lk(tid_mu);
+        s.insert((int)syscall(SYS_gettid));
+    };
     const int per_side = coalesce ? threads : 1;
     for (int pi = 0; pi < pairs; ++pi)
       for (int ti = 0; ti < per_side; ++ti) {
         Pair& p = P[pi];
         th.emplace_back([&, pi, ti] {   // sender
             (void)prctl(PR_SET_TIMERSLACK, 1UL, 0, 0, 0);   // paced writers wake on time
+            note_tid(writer_tids);
             std::vector<uint8_t> buf((size_t)batch * len);
             std::vector<hyobfs_dgram> d(batch);
             std::vector<mmsghdr> mh(batch);
@@ -181,10 +231,13 @@ int main(int argc, char** argv) {
                 if (share > 0) {   // send what is due by now, up to a batch
                     const uint64_t now = now_ns();
                     const uint64_t want = (uint64_t)((double)(now - t_start) * share * 1e-9);
-                    if (want <= issued) {   // sleep until the next datagram is due (few wakeups)
+                    if (want <= issued) {   // sleep until the next datagram is due, at least
+                        // kMinSleepNs: a wakeup per datagram would cost the writer a core at
+                        // 250 k datagrams/s and eat the box's CPU quota (what is due after a
+                        // longer sleep goes out together, stamped when each is sent)
                         const double next_ns = (double)(issued + 1) / share * 1e9 + (double)t_start;
                         const double gap = next_ns - (double)now;
-                        std::this_thread::sleep_for(std::chrono::nanoseconds((int64_t)std::max(gap, 2000.0)));
+                        std::this_thread::sleep_for(std::chrono::nanoseconds((int64_t)std::max(gap, kMinSleepNs)));
                         continue;
                     }
                     nb = (uint32_t)std::min<uint64_t>(want - issued, batch);
@@ -213,6 +266,7 @@ int main(int argc, char** argv) {
             }
         });
         th.emplace_back([&] {   // receiver
+            note_tid(reader_tids);
             std::vector<uint8_t> buf((size_t)batch * 2048);
             std::vector<hyobfs_dgram> d(batch);
             std::vector<mmsghdr> mh(batch);
@@ -265,15 +319,40 @@ int main(int argc, char** argv) {
     cg_throttle(thr_n0, thr_us0);
     rusage ru0{}, ru1{};
     getrusage(RUSAGE_SELF, &ru0);
+    const auto tc0 = task_cpu();
     uint64_t r0 = 0, s0 = 0;
     for (auto& p : P) r0 += p.recvd, s0 += p.sent;
+    // coalescing counters (hyobfs_conn_stats: [1] tx batches, [4] rx batches) over the window
+    auto batches = [&](uint64_t& txb, uint64_t& rxb) {
+        txb = rxb = 0;
+        for (auto& p : P) {
+            uint64_t st[6] = {};
+            if (coalesce && hyobfs_conn_stats(p.sc, st) == HYOBFS_OK) txb += st[1];
+            if (coalesce && hyobfs_conn_stats(p.rc, st) == HYOBFS_OK) rxb += st[4];
+        }
+    };
+    uint64_t txb0, rxb0, txb1, rxb1;
+    batches(txb0, rxb0);
     const auto t0 = std::chrono::steady_clock::now();
     std::this_thread::sleep_for(std::chrono::duration<double>(seconds));
     uint64_t r1 = 0, s1 = 0;
     for (auto& p : P) r1 += p.recvd, s1 += p.sent;
+    batches(txb1, rxb1);
     const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     getrusage(RUSAGE_SELF, &ru1);
+    const auto tc1 = task_cpu();
     cg_throttle(thr_n1, thr_us1);
+    // cores used per thread class over the window: the bench's writers and readers, and
+    // every other thread (the library's coalescer threads, the HIP runtime's) by name
+    const double hz = (double)sysconf(_SC_CLK_TCK);
+    std::map<std::string, double> by_class;
+    for (const auto& [tid, t1] : tc1) {
+        auto it = tc0.find(tid);
+        const uint64_t d = t1.ticks - (it != tc0.end() ? it->second.ticks : 0);
+        const std::string cls = writer_tids.count(tid) ? "bench_writers" : reader_tids.count(tid) ? "bench_readers"
+                                                                                                    : "other:" + t1.comm;
+        by_class[cls] += (double)d / hz;
+    }
     auto tv_s = [](const timeval& t) { return (double)t.tv_sec + 1e-6 * (double)t.tv_usec; };
     const double cpu_s = tv_s(ru1.ru_utime) - tv_s(ru0.ru_utime) + tv_s(ru1.ru_stime) - tv_s(ru0.ru_stime);
     stop = true;
@@ -295,14 +374,22 @@ int main(int argc, char** argv) {
         hyobfs_salamander_free(p.rctx);
     }
     const double rx = (double)(r1 - r0), tx = (double)(s1 - s0);
+    std::string cls_json;
+    for (const auto& [k, v] : by_class) {
+        char b[160];
+        snprintf(b, sizeof b, "%s\"%s\": %.2f", cls_json.empty() ? "" : ", ", k.c_str(), v / dt);
+        cls_json += b;
+    }
     printf("{\"mode\": \"%s\", \"offered_rate\": %.0f, \"pairs\": %d, \"threads_per_side\": %d, \"wait_us\": %u, \"len\": %u, \"batch\": %u, \"seconds\": %.3f, "
            "\"rx_datagrams_per_s\": %.0f, \"tx_datagrams_per_s\": %.0f, \"rx_payload_GiB_s\": %.4f, "
            "\"tx_payload_GiB_s\": %.4f, \"loss_frac\": %.4f, \"bad\": %llu, \"avg_per_read\": %.1f, "
            "\"latency_us_p50\": %.1f, \"latency_us_p99\": %.1f, \"latency_samples\": %zu, "
-           "\"cpu_cores_used\": %.2f, \"cgroup_throttled_periods\": %llu, \"cgroup_throttled_ms\": %.1f}\n",
+           "\"cpu_cores_used\": %.2f, \"cgroup_throttled_periods\": %llu, \"cgroup_throttled_ms\": %.1f, \"cpu_cores_by_thread\": {%s}, "
+           "\"tx_batches_per_s\": %.0f, \"rx_batches_per_s\": %.0f}\n",
            mode.c_str(), rate, pairs, per_side, coalesce ? wait_us : 0u, len, batch, dt, rx / dt, tx / dt, rx * len / dt / (1u << 30), tx * len / dt / (1u << 30),
            sent ? 1.0 - (double)recvd / (double)sent : 0.0, (unsigned long long)bad,
            calls ? (double)recvd / (double)calls : 0.0, pct(0.5), pct(0.99), lat.size(), cpu_s / dt,
-           (unsigned long long)(thr_n1 - thr_n0), (double)(thr_us1 - thr_us0) / 1e3);
+           (unsigned long long)(thr_n1 - thr_n0), (double)(thr_us1 - thr_us0) / 1e3, cls_json.c_str(),
+           (double)(txb1 - txb0) / dt, (double)(rxb1 - rxb0) / dt);
     return bad ? 1 : 0;
 }
