@@ -57,8 +57,12 @@ constexpr uint32_t kFGuard = 32;         // LDS bytes on both sides of the stage
 // salts between them (deobfuscate: 8 per datagram of a pass), plus 16-byte rounding
 template <bool OBF>
 constexpr uint32_t flat_stage_bytes() { return kFT + (OBF ? 32u : 8u * kFD + 32u); }
+// waves per SIMD the register budget is sized for: 7 (72 VGPRs) -- LDS allows about 8
+// workgroups per CU anyway, and at 8 (64 VGPRs) the tile path spilled 21-31 VGPRs;
+// 7 / 6 / 5 ran configs[2] in 1.541 / 1.597 / 1.665 ms against 1.640 at 8
+// (profiles/r06_bimodal/ab_flat_vgpr_cap.txt)
 #ifndef HY_FLAT_MIN_WAVES
-#define HY_FLAT_MIN_WAVES 8
+#define HY_FLAT_MIN_WAVES 7
 #endif
 // w[] flag bits above the width (widths are < 2^24)
 constexpr uint32_t kFlatOffWin = 1u << 31;   // some payload byte of the tile lies outside the staged window
@@ -447,7 +451,7 @@ __global__ __launch_bounds__(kFThreads, HY_FLAT_MIN_WAVES) void salamander_flat_
 #pragma unroll
             for (int w = 0; w < 4; ++w) {
                 kw[w] = tg[w] = 0;
-                if (live) krec_load(kb, (uint32_t)(kKeyRec * lane + 16 * w), kw[w], tg[w]);
+                if (live && F.nhash) krec_load(kb, (uint32_t)(kKeyRec * lane + 16 * w), kw[w], tg[w]);
             }
             uint32_t W = live ? out_width<OBF>(L, B.pkt_cap) : 0u;
             // tile-relative 32-bit scans: a pass spans at most 64 x 2^24 bytes
@@ -460,9 +464,11 @@ __global__ __launch_bounds__(kFThreads, HY_FLAT_MIN_WAVES) void salamander_flat_
             const int32_t orel = (int32_t)((int64_t)o - (int64_t)tT);
             const int32_t dlt = (int32_t)((int64_t)(i + SKIP) - (int64_t)ws) - (orel + SALT);
             // ---- keys: the hashers' records; a record not published yet is polled a
-            // while, then the wave hashes the pass's keys itself (four lanes per key)
+            // while, then the wave hashes the pass's keys itself (four lanes per key;
+            // at once when the launch has no hashers)
             bool miss = W && (tg[0] != F.epoch || tg[1] != F.epoch || tg[2] != F.epoch || tg[3] != F.epoch);
-            for (int spin = 0; spin < 48 && __ballot(miss); ++spin) {
+            const int spins = F.nhash ? 48 : 0;
+            for (int spin = 0; spin < spins && __ballot(miss); ++spin) {
 #ifndef HYOBFS_EMULATE
                 __builtin_amdgcn_s_sleep(8);
 #endif

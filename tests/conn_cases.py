@@ -387,6 +387,39 @@ def run_rx_gpu_failure_scenario(device: int = 0, max_batch: int = 16):
         orecv.close()
 
 
+def run_tx_gpu_failure_scenario(device: int = 0, max_batch: int = 16):
+    """A send batch whose GPU step fails (CPU tier only: HYEMU_FAIL_EVENTS_FROM=1 fails
+    every event of the connection's queues, the sleep-polling wait's hipEventQuery
+    included).  WriteTo had already returned len(p): the datagram is counted as a tx
+    error and is not sent (nothing unobfuscated reaches the socket), and the next
+    WriteTo raises EIO once -- the reference returns the error of conn.go:93-98 to the
+    caller whose datagram failed, which a queued send cannot do (include/hyobfs_conn.h)."""
+    oa = SalamanderObfuscator(PSK, device)
+    raw = _udp()
+    raw.settimeout(0.5)
+    r_addr = raw.getsockname()
+    ca = SalamanderPacketConn(_udp(), oa, batch=max_batch)
+    try:
+        ca.set_coalescing(max_batch, 50)
+        assert ca.write_to(b"x" * 100, r_addr) == 100
+        ca.flush()
+        assert ca.stats()["tx_errors"] == 1, ca.stats()
+        try:
+            ca.write_to(b"y", r_addr)
+            raise AssertionError("a failed send batch was not reported")
+        except OSError as e:
+            assert e.errno == errno.EIO, e
+        try:
+            raw.recvfrom(4096)
+            raise AssertionError("a datagram whose GPU step failed reached the socket")
+        except socket.timeout:
+            pass
+    finally:
+        ca.close()
+        raw.close()
+        oa.close()
+
+
 def _free_unclosed_closes_fd(oa, r_addr, raw, max_batch):
     """hyobfs_conn_wrap on a dup'd descriptor, hyobfs_conn_free with no
     hyobfs_conn_close first (include/hyobfs_conn.h): the fd leaves the process's

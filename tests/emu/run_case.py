@@ -443,6 +443,10 @@ if __name__ == "__main__":
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         from conn_cases import run_rx_gpu_failure_scenario
         run_rx_gpu_failure_scenario()
+    elif which == "txfail":   # run with HYEMU_FAIL_EVENTS_FROM=1 (tests/emu/hip_emu.h)
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        from conn_cases import run_tx_gpu_failure_scenario
+        run_tx_gpu_failure_scenario()
     elif which == "closerace":
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         from conn_cases import run_close_race_scenarios

@@ -49,6 +49,7 @@ SPECS = {
     "test_emulated_split_launches": lambda p: (p["which"], p["args"], dict(p["env"])),
     "test_emulated_contiguous_input_slotted": lambda p: ("contig", p["args"], {"HYEMU_CUS": "2"}),
     "test_emulated_rx_gpu_failure_reports_eio": lambda p: ("rxfail", "", {"HYEMU_FAIL_EVENTS_FROM": "5"}),
+    "test_emulated_tx_gpu_failure_reports_eio": lambda p: ("txfail", "", {"HYEMU_FAIL_EVENTS_FROM": "1"}),
     "test_emulated_contiguous_input_auto": lambda p: ("contig", p["args"], {"HYEMU_CUS": "2"}),
     "test_emulated_contiguous_input_flat": lambda p: ("contig", p["args"], {"HYEMU_CUS": "2", "HYOBFS_KERNEL": "flat",
                                                                            "HYOBFS_FLAT_HASHERS": p["hashers"]}),
@@ -294,3 +295,10 @@ def test_emulated_rx_gpu_failure_reports_eio(emu_lib):
     (once per failed batch) and nothing is counted as an invalid datagram (rx_dropped 0);
     the emulation fails every wait of the receive queue (HYEMU_FAIL_EVENTS_FROM=5)."""
     _run(emu_lib, "rxfail", "", {"HYEMU_FAIL_EVENTS_FROM": "5"})
+
+
+def test_emulated_tx_gpu_failure_reports_eio(emu_lib):
+    """A coalescing connection's send batch whose GPU step fails: the datagram is not
+    sent, it counts as a tx error, and the next WriteTo raises EIO once (every event of
+    the connection fails, HYEMU_FAIL_EVENTS_FROM=1)."""
+    _run(emu_lib, "txfail", "", {"HYEMU_FAIL_EVENTS_FROM": "1"})
