@@ -43,17 +43,8 @@ __device__ __forceinline__ gk_u128 gk_mask(uint32_t lo, uint32_t hi) {   // byte
     return m << (8 * lo);
 }
 
-#ifndef HY_GK_PIPE
-#define HY_GK_PIPE 1   // software-pipelined aligned sweep (two iterations' loads in flight)
-#endif
 #ifndef HY_GK_U
 #define HY_GK_U 3   // 4 spills at the 5-wave register cap
-#endif
-#ifndef HY_GK_MERGE
-#define HY_GK_MERGE 1   // aligned sweep: padding and message chunks leave through one conditional store
-#endif
-#ifndef HY_GK_EDGE_KS
-#define HY_GK_EDGE_KS 1   // edge chunks' padding keystream computed up front, a column per lane (not inside the edge loop)
 #endif
 constexpr int kGkU = HY_GK_U;   // windows per lane in flight
 
@@ -70,10 +61,8 @@ struct GeckoGroup {             // one wave's 64 frames, in LDS
     uint32_t hp_plain[64];      // chunk start (low 16 bits) | plaintext length (high 16 bits)
     uint64_t salt[64];          // aligned path: the salts (merged into the edge chunks)
     gk_u128 key[128];           // the frame's key, two halves (aligned path: rotated to the wire phase)
-#if HY_GK_EDGE_KS
     gk_u128 eks[128];           // aligned path: keystream of frame k's edge chunks holding padding
                                 // ([2k] the pad's first chunk, [2k + 1] its last)
-#endif
 };
 
 // The 5 header bytes of frame k, little-endian in the low bytes (encodeFrame,
@@ -199,14 +188,9 @@ __device__ __forceinline__ void gk_contrib(const hyobfs_gecko_batch& B, const Gk
         }
         const int32_t plo = max(p0, (int32_t)HYOBFS_GECKO_HEADER_LEN), phi = min(p0 + 16, hp);
         if (plo < phi) {   // the 16-aligned wire chunk at base + a is one keystream column
-#if HY_GK_EDGE_KS
             // an edge chunk holding padding is the pad's first or last chunk (precomputed)
             const uint32_t c0 = (rs + HYOBFS_SALT_LEN + HYOBFS_GECKO_HEADER_LEN) >> 4;
             X |= G.eks[2 * k + ((a >> 4) == c0 ? 0u : 1u)] & gk_mask(plo - p0, phi - p0);
-#else
-            X |= gk_ks_single(P, (base + a) >> 6, (uint32_t)((base + a) >> 4) & 3u) &
-                 gk_mask(plo - p0, phi - p0);
-#endif
         }
         const int32_t clo = max(p0, hp);
         if (clo < xhi) {   // chunk bytes
@@ -259,7 +243,6 @@ __device__ __forceinline__ void gecko_encode_aligned(const KeyParams& K, const h
         G.key[2 * lane + 1] = (gk_u128)kr[3] << 64 | kr[2];
         G.salt[lane] = salt;
     }
-#if HY_GK_EDGE_KS
     // ---- the keystream columns of the edge chunks that hold padding: frame l's pad
     // runs over wire [rs + 13, rs + 8 + hp); its first and last chunk are edges unless
     // wholly padding (then the sweep covers them).  One column per lane, 64 per pass
@@ -285,7 +268,6 @@ __device__ __forceinline__ void gecko_encode_aligned(const KeyParams& K, const h
             if (c != ~0u) G.eks[n] = gk_ks_single(P, (base + 16ull * c) >> 6, c & 3u);
         }
     }
-#endif
     hy_wave_sync();
     uint8_t* __restrict__ ob = B.out + base;
     const uint32_t tc = (rend + 15) >> 4;   // chunks of the group's wire range
@@ -367,7 +349,6 @@ __device__ __forceinline__ void gecko_encode_aligned(const KeyParams& K, const h
             S.v[u] = gk_load16u(msg ? B.msg + co + (uint32_t)(p - hp) : safe);
         }
     };
-#if HY_GK_MERGE
     auto retire = [&](uint32_t T, Step& S) {
 #pragma unroll
         for (int u = 0; u < kGkU; ++u) {
@@ -383,26 +364,7 @@ __device__ __forceinline__ void gecko_encode_aligned(const KeyParams& K, const h
             if (S.kind[u]) store16_stream(ob + 16 * c, S.v[u] ^ G.key[2 * S.kq[u] + (c & 1)]);
         }
     };
-#else
-    auto retire = [&](uint32_t T, const Step& S) {
-#pragma unroll
-        for (int u = 0; u < kGkU; ++u) {
-            const bool pad = S.kind[u] == 1;
-            if (__ballot(pad)) {   // the whole wave: a quad computes one 64-byte block
-                const uint32_t c = T + lane + 64 * u;
-                const gk_u128 ks = gk_ks_quad(P, (base + 16ull * c) >> 6, lane & 3u);
-                if (pad) store16_stream(ob + 16 * c, ks ^ G.key[2 * S.kq[u] + (c & 1)]);
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < kGkU; ++u) {
-            const uint32_t c = T + lane + 64 * u;
-            if (S.kind[u] == 2) store16_stream(ob + 16 * c, S.v[u] ^ G.key[2 * S.kq[u] + (c & 1)]);
-        }
-    };
-#endif
     constexpr uint32_t STEP = 64 * kGkU;
-#if HY_GK_PIPE
     // Software pipelined: iteration i+1's loads are issued before iteration i's
     // stores, so waiting for them never waits for those stores (vmcnt counts loads
     // and stores in issue order); past the range end issue() reads only the safe line.
@@ -417,13 +379,6 @@ __device__ __forceinline__ void gecko_encode_aligned(const KeyParams& K, const h
             retire(T + STEP, S1);
         }
     }
-#else
-    for (uint32_t T = 0; T < tc; T += STEP) {
-        Step S;
-        issue(T, S);
-        retire(T, S);
-    }
-#endif
 }
 
 // Register cap: 5 waves/SIMD with the pipelined sweep (two iterations' registers):

@@ -235,15 +235,12 @@ __device__ __forceinline__ void store16_global(uint8_t* p, uint64_t lo, uint64_t
 }
 
 // The wire salt the key wave reads while the DMA waves stage the same line
-// (deobfuscate).  HY_TILE_WIRE_SALT 1 (default): a temporal load, so the line is
-// allocated in L2 and the DMA's request for it hits there; 0: non-temporal, which
-// fetched those lines twice from HBM (uniform deobfuscate: reads 1.042 x the input
-// against 1.0016 x, 0.4181 against 0.3962 ms per launch, profiles/r04_ab_uniform_saltt.txt)
-#ifndef HY_TILE_WIRE_SALT
-#define HY_TILE_WIRE_SALT 1
-#endif
+// (deobfuscate): a temporal load, so the line is allocated in L2 and the DMA's request
+// for it hits there; a non-temporal load fetched those lines twice from HBM (uniform
+// deobfuscate: reads 1.042 x the input against 1.0016 x, 0.4181 against 0.3962 ms per
+// launch, profiles/r04_ab_uniform_saltt.txt)
 __device__ __forceinline__ uint64_t load8_wire_salt(const uint8_t* p) {   // 8-aligned
-#if HY_TILE_WIRE_SALT == 0 || defined(HYOBFS_EMULATE)
+#ifdef HYOBFS_EMULATE
     return load8_nt(p);
 #else
     typedef uint32_t v2u __attribute__((ext_vector_type(2)));
