@@ -272,7 +272,7 @@ static uint64_t next_epoch() {
 // The flat kernel (salamander_flat.h) runs when asked for (HYOBFS_KERNEL_FLAT, or
 // HYOBFS_KERNEL=flat) on contiguous input into packed output from 16-byte aligned
 // input.  AUTO keeps the wave kernel there: on configs[2] it is faster (1.36-1.42 ms
-// against 1.56-1.68 ms for the flat kernel's best variants, profiles/r06_bimodal/).
+// against 1.53-1.68 ms for the flat kernel's variants, profiles/r06_bimodal/).
 static bool flat_eligible(const BatchParams& b) {
     return contiguous_input(b) && b.out_stride == 0 && resolve_kernel(b.kernel) == kKernelFlat &&
            (reinterpret_cast<uintptr_t>(b.in) & 15u) == 0;
