@@ -222,24 +222,16 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t x) {
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
-// A streamed output chunk: a non-temporal vector store with system-coherence scope
-// (nt sc1), which drops the line from the XCD's L2 once written (MI355X_MICROARCH.md,
-// store flavours) and leaves the L2 to the input lines that neighbouring chunks still
-// read: configs[2] on the wave kernel 1.2 % (obfuscate) / 2.0 % (deobfuscate) faster than
-// nt alone, Gecko unchanged (profiles/r06_ab_stream_store_ntsc1*.txt, r06_ab_stream_store_nop.txt).
-// No builtin emits these cache bits on a global store, hence the inline store; the
-// compiler does not see it read its data registers, so the asm itself waits out the
-// wide-store data hazard (s_nop 1: two wait states before any instruction can overwrite
-// them).  Without that wait the flat kernel's output lost a dword per chunk
-// (profiles/r06_diag_store_policy/).  The tile kernel's staged stores (store16_global)
-// measured the same either way and stay nt.
+#ifndef HY_NT_STORES
+#define HY_NT_STORES 1
+#endif
 __device__ __forceinline__ void store16_stream(uint8_t* dst, u128 r) {   // dst 16-aligned
     u32x4 v;
     __builtin_memcpy(&v, &r, 16);
-#ifdef HYOBFS_EMULATE
+#if HY_NT_STORES
     __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(dst));
 #else
-    asm volatile("global_store_dwordx4 %0, %1, off nt sc1\n\ts_nop 1" ::"v"(dst), "v"(v) : "memory");
+    *reinterpret_cast<u32x4*>(dst) = v;
 #endif
 }
 
